@@ -1,0 +1,212 @@
+/*
+ * ofdm_mi355x.h — C-ABI of the MI355X-native OFDM modem core.
+ *
+ * This is the drop-in boundary for the reference's DSP layer (DmSM-1/C-OFDM,
+ * OFDM/Frame.{hpp,cpp} + OFDM/modulation.{hpp,cpp} + config/parser.{hpp,cpp}).
+ * The reference exposes a C++ class surface and no C ABI; each
+ * entry point below names the reference member it replaces (file:line,
+ * relative to the reference root). The C++ compatibility layer in
+ * c-ofdm_amd/compat/ re-exposes that class surface on top of these calls.
+ *
+ * Conventions
+ *   - Every function returns an int status: OFDM_OK (0) or a negative
+ *     OFDM_ERR_* code; ofdm_last_error() gives a thread-local message.
+ *   - Complex samples are interleaved FP64 {re, im} (the std::complex<double>
+ *     layout of the reference and of its data/*.bin files).
+ *   - Batched compute entry points take DEVICE pointers and an explicit HIP
+ *     stream passed as void* (NULL = the legacy default stream). They are
+ *     asynchronous; they never allocate, copy to the host or synchronise, so
+ *     they can be captured into a hipGraph.
+ *   - One ofdm_ctx per thread (or per GPU); a ctx is not re-entrant, matching
+ *     the reference (one FRAME_FORM per thread).
+ */
+#ifndef OFDM_MI355X_H
+#define OFDM_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OFDM_MI355X_ABI_VERSION 1
+
+enum {
+    OFDM_OK = 0,
+    OFDM_ERR_INVALID = -1,     /* bad argument / geometry the kernels do not cover */
+    OFDM_ERR_UNSUPPORTED = -2, /* valid reference config this build does not run   */
+    OFDM_ERR_HIP = -3,         /* HIP runtime error (no GPU, launch failure, ...)  */
+    OFDM_ERR_IO = -4,          /* config/file I/O (reference throws runtime_error) */
+    OFDM_ERR_NOMEM = -5,
+    OFDM_ERR_PARSE = -6        /* std::stol failure in parse_config                */
+};
+
+/*
+ * Flat view of the ConfigMap keys the hot path consumes
+ * (config/parser.hpp:8, consumed in OFDM/Frame.cpp:99-118,157-176,213-232,259-273).
+ * Integer-coded fixed point is kept as in config.txt: pilot_ampl/1000,
+ * pr_level/1000, t2_sin_level/1000. Missing keys read as 0, as with the
+ * reference's ConfigMap::operator[].
+ */
+typedef struct ofdm_params {
+    long fft_size;       /* N */
+    long num_data_subc;  /* D */
+    long num_pilot_subc; /* P */
+    long cp_size;
+    long num_symb;       /* message symbols per frame */
+    long num_pr_symb;    /* preamble symbols */
+    long pr_sin_len;     /* preamble correlation template length */
+    long pr_seed;        /* std::mt19937 seed of the preamble bytes */
+    long pr_level;       /* /1000: preamble detection threshold */
+    long t2sin_size;     /* T2 marker length = detector block */
+    long t2_sin_f1;
+    long t2_sin_f2;
+    long t2_sin_level;   /* /1000: T2 energy-ratio threshold */
+    long smooth;         /* T2 mask half-width */
+    long mod_type;       /* bits per symbol: 1 bpsk, 2 qam4, 4 qam16, 6 qam64, 8 qam256 */
+    long pilot_ampl;     /* /1000: transmitted pilot amplitude */
+    long mult;           /* int16 wire scaling (FRAME_FORM::get_int16) */
+    long rx_buf_size;    /* rx ring = frame * (rx_buf_size + 1) */
+    long iterations;     /* rx.cpp loop count (not used by the core) */
+} ofdm_params;
+
+/* Derived frame geometry (FRAME_FORM ctor, OFDM/Frame.cpp:213-232). */
+typedef struct ofdm_geometry {
+    long symbol_len;       /* N + cp (OFDM_FORM::ofdm_len)                       */
+    long message_len;      /* (N+cp)*num_symb  (message.size)                   */
+    long preamble_len;     /* (N+cp)*num_pr_symb (preamble.size)                */
+    long frame_len;        /* T2 + preamble + message (FRAME_FORM::output_size) */
+    long ring_len;         /* frame_len*(rx_buf_size+1) (from_sdr_buf.size())   */
+    long data_per_frame;   /* D*num_symb constellation points (message.usefull_size) */
+    long bytes_per_frame;  /* D*num_symb*k/8 (FRAME_FORM::usefull_size)         */
+    long segment_size;     /* D/P data carriers between pilots                  */
+    long pilot_bin[256];   /* pilot FFT bins of one symbol (first P entries)    */
+    long segment_bin[256]; /* first FFT bin of each data segment                */
+} ofdm_geometry;
+
+/* Optional AWGN channel fused into the tx kernel (bench/loopback only; the
+ * reference's channel is the radio, python_code/channel.py). Counter-based
+ * noise: identical sample index -> identical noise on every GPU/rank. */
+typedef struct ofdm_channel {
+    double noise_std;        /* std of the complex noise per time sample (total power) */
+    unsigned long long seed;
+    unsigned long long sample_offset; /* global index of this batch's first sample */
+} ofdm_channel;
+
+typedef struct ofdm_ctx ofdm_ctx;
+
+/* ---- errors / version -------------------------------------------------- */
+const char* ofdm_last_error(void);
+int ofdm_abi_version(void);
+
+/* ---- config (config/parser.cpp:4-33, config/config.txt) ---------------- */
+/* The committed config/config.txt values. */
+int ofdm_params_default(ofdm_params* out);
+/* parse_config(path) + the config["..."] lookups of the Frame ctors.
+ * Returns OFDM_ERR_IO if the file cannot be opened ("Cannot open config
+ * file"), OFDM_ERR_PARSE where std::stol would throw. Unknown keys ignored. */
+int ofdm_params_from_config(const char* path, ofdm_params* out);
+/* Read one raw key the way ConfigMap::operator[] would (0 when missing). */
+int ofdm_config_lookup(const char* path, const char* key, long* value);
+
+/* ---- context ----------------------------------------------------------- */
+/* Builds every constant the FRAME_FORM ctor builds (Frame.cpp:213-232):
+ * pilot/segment tables (Frame.cpp:31-44), T2 marker (Frame.cpp:139-154),
+ * preamble bytes/symbol/template (Frame.cpp:259-294), T2 mask (Frame.cpp:120-133),
+ * FFT twiddle tables; uploads them to `device`. */
+int ofdm_create(const ofdm_params* params, int device, ofdm_ctx** out);
+int ofdm_destroy(ofdm_ctx* ctx);
+int ofdm_get_geometry(const ofdm_ctx* ctx, ofdm_geometry* out);
+/* Host copies of the constant frame parts (for FRAME_FORM::buf, get(), preamble.*). */
+int ofdm_get_t2_symbol(const ofdm_ctx* ctx, double* out /* t2sin_size complex */);
+int ofdm_get_preamble(const ofdm_ctx* ctx,
+                      uint8_t* bytes_out /* D*num_pr_symb/8, nullable */,
+                      double* ofdm_preamble_out /* preamble_len complex, nullable */,
+                      double* mod_preamble_out /* D*num_pr_symb complex, nullable */,
+                      double* template_out /* pr_sin_len complex, nullable */);
+
+/* ---- device memory helpers (so hosts need not link HIP) ----------------- */
+int ofdm_device_alloc(ofdm_ctx* ctx, size_t bytes, void** dptr);
+int ofdm_device_free(ofdm_ctx* ctx, void* dptr);
+int ofdm_memcpy_h2d(ofdm_ctx* ctx, void* dst, const void* src, size_t bytes, void* stream);
+int ofdm_memcpy_d2h(ofdm_ctx* ctx, void* dst, const void* src, size_t bytes, void* stream);
+int ofdm_memset_device(ofdm_ctx* ctx, void* dst, int value, size_t bytes, void* stream);
+int ofdm_stream_synchronize(ofdm_ctx* ctx, void* stream);
+
+/* ---- tx: FRAME_FORM::write (Frame.cpp:235-237) -> OFDM_FORM::write
+ *      (Frame.cpp:185-198) -> Modulation::mod (modulation.cpp:39-50) +
+ *      FFT_FORM::write (Frame.cpp:54-70), batched over frames ------------- */
+/* bytes: nframes * bytes_per_frame (device). iq_out: device, frame f's
+ * message starts at iq_out + 2*f*frame_stride (complex samples; stride >=
+ * message_len). Each symbol is [CP | body], body = IFFT(pilots+data)/sqrt(N).
+ * iq16_out (nullable, device): the same samples as complex<int16>
+ * trunc(x*mult) — FRAME_FORM::get_int16 (Frame.cpp:249-256), same stride.
+ * ch (nullable, host struct): AWGN added to iq_out only. */
+int ofdm_tx_modulate(ofdm_ctx* ctx, const uint8_t* bytes, size_t nframes,
+                     double* iq_out, size_t frame_stride, int16_t* iq16_out,
+                     const ofdm_channel* ch, void* stream);
+
+/* Full FRAME_FORM buffers: [T2 | preamble | message] per frame (output_size
+ * samples, contiguous frames), i.e. what FRAME_FORM::get() returns. */
+int ofdm_tx_frames(ofdm_ctx* ctx, const uint8_t* bytes, size_t nframes,
+                   double* frames_out, int16_t* frames16_out, void* stream);
+
+/* ---- rx: OFDM_FORM::fft (Frame.hpp:276-282) -> FFT_FORM::read
+ *      (Frame.cpp:73-96) [-> caller's constell /= chan (main.cpp:69-71)]
+ *      -> Modulation::demod (modulation.cpp:53-87), batched over frames ---- */
+/* iq: device, frame f's message (num_symb [CP|body] symbols) at
+ * iq + 2*f*frame_stride. chan (nullable, device): per-frame D complex
+ * divisors (chan_stride complex between frames; 0 = one shared vector).
+ * constell_out (nullable): nframes*D*num_symb complex, equalised points
+ * BEFORE demod's clamp (data/constell.bin layout). bytes_out (nullable):
+ * nframes*bytes_per_frame. ref_bytes + bit_errors (both nullable, device):
+ * accumulate popcount(bytes ^ ref_bytes) into *bit_errors (u64 atomic). */
+int ofdm_rx_demod(ofdm_ctx* ctx, const double* iq, size_t nframes, size_t frame_stride,
+                  const double* chan, size_t chan_stride,
+                  double* constell_out, uint8_t* bytes_out,
+                  const uint8_t* ref_bytes, unsigned long long* bit_errors,
+                  void* stream);
+
+/* Modulation::demod alone on n points (modulation.cpp:53-87): clamps `points`
+ * IN PLACE for QAM (as the reference does) and writes n*k/8 bytes (rounded up,
+ * last byte left-aligned as bit_stream_converter pads). Device pointers. */
+int ofdm_demap(ofdm_ctx* ctx, double* points, size_t n, uint8_t* bytes_out, void* stream);
+/* Modulation::mod alone (modulation.cpp:39-50): nbytes -> nbytes*8/k points. */
+int ofdm_map(ofdm_ctx* ctx, const uint8_t* bytes, size_t nbytes, double* points_out, void* stream);
+
+/* ---- rx sync front end ----------------------------- */
+/* T2SIN_FORM::corr (Frame.hpp:96-147) over all floor((n-start)/t2sin_size)
+ * blocks from `start`: rel_out[b] = energy ratio if > level else 0 (device,
+ * nullable). first_out (device int, nullable): T2SIN_FORM::find_t2sin
+ * (Frame.hpp:150-197) = start + b*size of the first block above level, or -1. */
+int ofdm_t2_scan(ofdm_ctx* ctx, const double* iq, size_t n, long start,
+                 double* rel_out, int* first_out, void* stream);
+
+/* PREAMBLE_FORM::find_preamble (Frame.cpp:338-378) for a batch of starts:
+ * idx_out[i] = first lag index (start_i + lag) whose normalised
+ * correlation exceeds pr_level/1000, or -10. Device arrays. */
+int ofdm_find_preamble(ofdm_ctx* ctx, const double* iq, size_t n,
+                       const int* starts, size_t nstarts, int* idx_out, void* stream);
+
+/* Per-frame synchronisation of a located frame, in place on the
+ * message_with_preamble region (preamble + message, (N+cp)*(num_pr_symb+num_symb)
+ * samples at frames + f*frame_stride):
+ *   cfo = OFDM_FORM::pilot_freq_sinh   (Frame.hpp:285-337)  -> cfo_out[f]
+ *   OFDM_FORM::freq_shift(cfo)         (Frame.hpp:340-348)
+ *   OFDM_FORM::cp_freq_sinh            (Frame.hpp:238-263)
+ *   OFDM_FORM::pr_phase_sinh(ofdm_preamble) (Frame.hpp:265-274)
+ *   PREAMBLE_FORM::chan_char_lq        (Frame.hpp:389-434) -> chan_out[f*D]
+ * Any of `stages` bits may be cleared to skip a stage (OFDM_SYNC_* below). */
+enum {
+    OFDM_SYNC_CFO = 1, OFDM_SYNC_FREQ_SHIFT = 2, OFDM_SYNC_CP = 4,
+    OFDM_SYNC_PHASE = 8, OFDM_SYNC_CHAN = 16, OFDM_SYNC_ALL = 31
+};
+int ofdm_sync_frames(ofdm_ctx* ctx, double* frames, size_t nframes, size_t frame_stride,
+                     int stages, const double* cfo_in /* nullable: used when CFO stage is off */,
+                     double* cfo_out, double* chan_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OFDM_MI355X_H */
