@@ -1,0 +1,241 @@
+#!/usr/bin/env python3
+"""bench.py — IQ-samples/s of the MI355X OFDM modem hot path (BASELINE.json).
+
+Workload (BASELINE.json configs[1]): per GPU a batch of
+65 536 OFDM symbols = 8 192 frames x 8 symbols, N=2048, D=1024 data + 32
+pilots, cp=512, QPSK. One step = tx (map + pilot comb + IFFT + CP, fused
+counter-based AWGN at Es/N0 = 10 dB) then rx (CP strip + FFT + pilot
+normalise/equalise + demap + bit-error count) over the whole batch, inputs
+resident in HBM. value = IQ samples through the tx->rx loopback per second,
+whole job (all ranks). Multi-GPU: frames shard across ranks (weak scaling, no
+data-path collective); one RCCL all-reduce of {bit errors, bits, samples,
+frames} and a MAX of the elapsed time at the end.
+
+Run: python bench.py [--gpus N --steps K --warmup W]; N>1 via
+torch.distributed.run (one process per GPU, RCCL over xGMI).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "c-ofdm_amd", "python"))
+
+METRIC = "IQ-samples/sec (tx IFFT+CP and rx FFT+equalise), 2048-subcarrier frames, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
+CONFIG_B = dict(fft_size=2048, num_data_subc=1024, num_pilot_subc=32, cp_size=512, num_symb=8,
+                num_pr_symb=1, pr_sin_len=128, pr_seed=42, pr_level=500, t2sin_size=256, t2_sin_f1=17,
+                t2_sin_f2=51, t2_sin_level=800, smooth=5, mod_type=2, pilot_ampl=2500, mult=200,
+                rx_buf_size=40, iterations=10000)
+
+
+def rx_bytes_per_symbol(p) -> int:
+    """rx reads 16*N (CP not read), writes 16*D constellation + D*k/8 bytes."""
+    N, D, k = p["fft_size"], p["num_data_subc"], p["mod_type"]
+    return 16 * N + 16 * D + D * k // 8
+
+
+def tx_bytes_per_symbol(p) -> int:
+    """tx reads D*k/8 bytes, writes 16*(N+cp)."""
+    return p["num_data_subc"] * p["mod_type"] // 8 + 16 * (p["fft_size"] + p["cp_size"])
+
+
+def load_pmc(workload: str):
+    """HBM traffic per rx launch from a committed rocprofv3 PMC summary
+    (profiles/pmc_rx_*.json, made by tools/pmc_traffic.py), or None."""
+    import glob
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_rx_*.json"))):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") == workload:
+            best = d
+    return best
+
+
+def cpu_baseline(p, data_host: np.ndarray, nframes_sample: int, noise_std: float, budget_s: float):
+    """Oracle (plain-C restatement) tx+AWGN+rx loopback on host cores, 1 thread,
+    on a bounded sample of the same workload. Reported beside the GPU number."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    g = O.geometry(p)
+    bpf = g["bytes_per_frame"]
+    done = 0
+    t0 = time.perf_counter()
+    while True:
+        for f in range(nframes_sample):
+            iq = O.tx_batch(p, data_host[f * bpf:(f + 1) * bpf], 1)
+            iq = O.awgn(iq, noise_std, seed=1, sample_offset=f * g["message_len"])
+            O.rx_batch(p, iq, 1, g["message_len"], ref=data_host[f * bpf:(f + 1) * bpf],
+                       want_constell=True)
+        done += nframes_sample
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    samples = done * g["message_len"]
+    return {"value": samples / el, "unit": "IQ-samples/s", "cores": 1, "kind": "port",
+            "sample": f"{done} frames of the same config-B workload (oracle/ofdm_oracle.c tx+AWGN+rx "
+                      f"loopback, 1 thread, own radix-4/2 FFT; FFTW absent), {el:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=8192, help="frames per GPU (8 symbols each)")
+    ap.add_argument("--snr-db", type=float, default=10.0)
+    ap.add_argument("--cpu-budget", type=float, default=8.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import ofdm_mi355x as M
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    p = dict(CONFIG_B)
+    modem = M.Modem(p, local)
+    geo = modem.geo
+    nf = args.frames
+    S = p["num_symb"]
+    msg = geo.message_len
+    bpf = geo.bytes_per_frame
+    npts = p["num_data_subc"] * S
+
+    # payload: seeded per rank (independent shards), resident in HBM
+    rng = np.random.default_rng(0x5EED + rank)
+    data_host = rng.integers(0, 256, nf * bpf, dtype=np.uint8)
+    data = torch.from_numpy(data_host).to(dev)
+    iq = torch.empty((nf * msg,), dtype=torch.complex128, device=dev)
+    cons = torch.empty((nf * npts,), dtype=torch.complex128, device=dev)
+    out = torch.empty((nf * bpf,), dtype=torch.uint8, device=dev)
+    errs = torch.zeros((1,), dtype=torch.int64, device=dev)
+    es = 2.0  # QPSK constellation energy (points +-1 +-1j)
+    noise_std = float(np.sqrt(es / 10 ** (args.snr_db / 10)))
+    stream = torch.cuda.current_stream(dev)
+
+    K, W = args.steps, args.warmup
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+
+    def step(i, events=None):
+        if events:
+            events[0].record(stream)
+        modem.tx(data, nf, iq, noise_std=noise_std, seed=1, sample_offset=rank * nf * msg, stream=stream)
+        if events:
+            events[1].record(stream)
+        modem.rx(iq, nf, constell_out=cons, bytes_out=out, ref=data, bit_errors=errs, stream=stream)
+        if events:
+            events[2].record(stream)
+
+    for i in range(W):
+        step(i)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    errs.zero_()
+    t0 = time.perf_counter()
+    for i in range(K):
+        step(i, ev[i])
+    # final BER/throughput reduction (the one collective of the path)
+    totals = torch.stack([errs[0], torch.tensor(K * nf * bpf * 8, device=dev),
+                          torch.tensor(K * nf * msg, device=dev), torch.tensor(K * nf, device=dev)])
+    if dist:
+        dist.all_reduce(totals)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    el_t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    elapsed = float(el_t.item())
+
+    tx_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+    rx_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+    tot = totals.cpu().numpy().astype(np.int64)
+    samples = int(tot[2])
+    value = samples / elapsed
+
+    rx_bytes = nf * S * rx_bytes_per_symbol(p)
+    tx_bytes = nf * S * tx_bytes_per_symbol(p)
+    achieved = rx_bytes / (rx_ms * 1e-3) / 1e9
+    workload = f"config2_B_N2048_D1024_P32_cp512_QPSK_{nf}frames_x8sym_per_gpu"
+    pmc = load_pmc(workload)
+
+    result = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "IQ-samples/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": elapsed / K * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": f"synthetic: seeded random payload per rank, counter-based AWGN Es/N0={args.snr_db:g} dB",
+        "config": {
+            "workload": workload,
+            "fft_size": p["fft_size"], "num_data_subc": p["num_data_subc"],
+            "num_pilot_subc": p["num_pilot_subc"], "cp_size": p["cp_size"], "num_symb": S,
+            "mod_type": p["mod_type"], "frames_per_gpu": nf, "symbols_per_gpu": nf * S,
+            "samples_per_step_per_gpu": nf * msg, "parallelism": f"frame-sharded x{world}",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "rx_kernel<11> (CP strip+FFT+equalise+demap)",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "algorithmic_bytes_per_launch": rx_bytes,
+            "avg_launch_ms": rx_ms,
+            "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
+        },
+        "rx_iq_samples_per_s": world * nf * msg / (rx_ms * 1e-3),
+        "tx_iq_samples_per_s": world * nf * msg / (tx_ms * 1e-3),
+        "tx_achieved_gbs": tx_bytes / (tx_ms * 1e-3) / 1e9,
+        "tx_avg_launch_ms": tx_ms,
+        "ber": float(tot[0]) / max(float(tot[1]), 1.0),
+        "bit_errors": int(tot[0]),
+        "frames": int(tot[3]),
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            result["cpu_baseline"] = cpu_baseline(p, data_host, 4, noise_std, args.cpu_budget)
+        except Exception as e:  # reported, not fatal: the GPU number stands alone
+            result["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    modem.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

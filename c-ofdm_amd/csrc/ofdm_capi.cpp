@@ -1,0 +1,690 @@
+// ofdm_capi.cpp — implementation of include/ofdm_mi355x.h (the C-ABI drop-in
+// boundary). Host side: config parsing, validation, the constant tables the
+// reference builds in its constructors, and kernel dispatch. Every compute
+// entry point launches HIP kernels; there is no CPU compute path.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cctype>
+#include <cmath>
+#include <complex>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <random>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/ofdm_mi355x.h"
+#include "ofdm_internal.hpp"
+
+using cd = std::complex<double>;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what)
+{
+    return fail(OFDM_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr)                                   \
+    do {                                                \
+        hipError_t _e = (expr);                         \
+        if (_e != hipSuccess) return hip_fail(_e, #expr); \
+    } while (0)
+
+int ilog2_exact(long n)
+{
+    if (n <= 0 || (n & (n - 1))) return -1;
+    int l = 0;
+    while ((1L << l) < n) ++l;
+    return l;
+}
+
+// key=value ConfigMap exactly as parse_config (config/parser.cpp:4-33):
+// trim, skip blank and '#' lines and lines without '=', strip every space
+// from key and value, std::stol the value (throws -> OFDM_ERR_PARSE).
+int parse_file(const char* path, std::unordered_map<std::string, long>& cfg)
+{
+    if (!path) return fail(OFDM_ERR_INVALID, "null config path");
+    std::ifstream file(path);
+    if (!file.is_open()) return fail(OFDM_ERR_IO, "Cannot open config file");
+    std::string line;
+    while (std::getline(file, line)) {
+        line.erase(line.begin(), std::find_if(line.begin(), line.end(),
+                                              [](unsigned char ch) { return !std::isspace(ch); }));
+        line.erase(std::find_if(line.rbegin(), line.rend(), [](unsigned char ch) { return !std::isspace(ch); })
+                       .base(),
+                   line.end());
+        if (line.empty() || line[0] == '#') continue;
+        auto pos = line.find('=');
+        if (pos == std::string::npos) continue;
+        std::string key = line.substr(0, pos), value = line.substr(pos + 1);
+        key.erase(std::remove_if(key.begin(), key.end(), ::isspace), key.end());
+        value.erase(std::remove_if(value.begin(), value.end(), ::isspace), value.end());
+        try {
+            cfg[key] = std::stol(value);
+        } catch (const std::exception& e) {
+            return fail(OFDM_ERR_PARSE, "stol failed for key '%s': %s", key.c_str(), e.what());
+        }
+    }
+    return OFDM_OK;
+}
+
+template <class T>
+int upload(T** dst, const std::vector<T>& v)
+{
+    HIP_TRY(hipMalloc((void**)dst, std::max<size_t>(1, v.size()) * sizeof(T)));
+    if (!v.empty()) HIP_TRY(hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return OFDM_OK;
+}
+
+}  // namespace
+
+// --------------------------------------------------------------------------
+struct ofdm_ctx {
+    ofdm_params p{};
+    int device = 0;
+    int logn = 0;
+    int N = 0, D = 0, P = 0, cp = 0, S = 0, k = 0, L = 0, seg = 0, npr = 0, t2 = 0;
+    ofdm_geometry geo{};
+    // host constants
+    std::vector<cd> t2_symbol, ofdm_preamble, mod_preamble, templ;
+    std::vector<uint8_t> preamble_bytes;
+    std::vector<double> t2_mask;
+    // device tables
+    double2* d_tw = nullptr;
+    int* d_data_bin = nullptr;
+    int* d_data_slot = nullptr;
+    int* d_pilot_bin = nullptr;
+    int* d_bin_map = nullptr;
+    double2* d_const = nullptr;
+    double2* d_const_bpsk = nullptr;
+    double2* d_header = nullptr;   // T2 + preamble
+    double2* d_preamble = nullptr; // ofdm_preamble (preamble_len)
+    double2* d_templ = nullptr;    // pr_sin_len
+    double2* d_modpre = nullptr;   // D*npr
+    double* d_t2mask = nullptr;    // t2 size
+    double2* d_t2tw = nullptr;     // t2-size twiddles (sync)
+    double2* d_prtw = nullptr;     // preamble-length twiddles (sync)
+    int sync_tables_ok = 0;
+    // staged-rx scratch (grown on demand, only for num_symb > 8 or D > N/2)
+    double2* d_scratch = nullptr;
+    size_t scratch_bytes = 0;
+
+    ofdm::DevTables tables(bool bpsk) const
+    {
+        ofdm::DevTables t;
+        t.tw = d_tw;
+        t.data_bin = d_data_bin;
+        t.data_slot = d_data_slot;
+        t.pilot_bin = d_pilot_bin;
+        t.bin_map = d_bin_map;
+        t.constell = bpsk ? d_const_bpsk : d_const;
+        return t;
+    }
+};
+
+extern "C" {
+
+const char* ofdm_last_error(void) { return g_err.c_str(); }
+int ofdm_abi_version(void) { return OFDM_MI355X_ABI_VERSION; }
+
+int ofdm_params_default(ofdm_params* o)
+{
+    if (!o) return fail(OFDM_ERR_INVALID, "null params");
+    *o = ofdm_params{};
+    o->fft_size = 512;
+    o->num_data_subc = 256;
+    o->num_pilot_subc = 8;
+    o->cp_size = 128;
+    o->num_symb = 8;
+    o->num_pr_symb = 1;
+    o->pr_sin_len = 128;
+    o->pr_seed = 42;
+    o->pr_level = 500;
+    o->t2sin_size = 256;
+    o->t2_sin_f1 = 17;
+    o->t2_sin_f2 = 51;
+    o->t2_sin_level = 800;
+    o->smooth = 5;
+    o->mod_type = 4;
+    o->pilot_ampl = 2500;
+    o->mult = 200;
+    o->rx_buf_size = 40;
+    o->iterations = 10000;
+    return OFDM_OK;
+}
+
+int ofdm_params_from_config(const char* path, ofdm_params* o)
+{
+    if (!o) return fail(OFDM_ERR_INVALID, "null params");
+    std::unordered_map<std::string, long> c;
+    int rc = parse_file(path, c);
+    if (rc) return rc;
+    // ConfigMap::operator[] semantics: missing keys read as 0
+    o->fft_size = c["fft_size"];
+    o->num_data_subc = c["num_data_subc"];
+    o->num_pilot_subc = c["num_pilot_subc"];
+    o->cp_size = c["cp_size"];
+    o->num_symb = c["num_symb"];
+    o->num_pr_symb = c["num_pr_symb"];
+    o->pr_sin_len = c["pr_sin_len"];
+    o->pr_seed = c["pr_seed"];
+    o->pr_level = c["pr_level"];
+    o->t2sin_size = c["T2sin_size"];
+    o->t2_sin_f1 = c["T2_sin_f1"];
+    o->t2_sin_f2 = c["T2_sin_f2"];
+    o->t2_sin_level = c["T2_sin_level"];
+    o->smooth = c["smooth"];
+    o->mod_type = c["modType"];
+    o->pilot_ampl = c["pilot_ampl"];
+    o->mult = c["mult"];
+    o->rx_buf_size = c["rx_buf_size"];
+    o->iterations = c["iterations"];
+    return OFDM_OK;
+}
+
+int ofdm_config_lookup(const char* path, const char* key, long* value)
+{
+    if (!key || !value) return fail(OFDM_ERR_INVALID, "null key/value");
+    std::unordered_map<std::string, long> c;
+    int rc = parse_file(path, c);
+    if (rc) return rc;
+    *value = c[key];
+    return OFDM_OK;
+}
+
+static int validate(const ofdm_params* p)
+{
+    const long N = p->fft_size, D = p->num_data_subc, P = p->num_pilot_subc, k = p->mod_type;
+    if (ilog2_exact(N) < 6 || ilog2_exact(N) > 12)
+        return fail(OFDM_ERR_UNSUPPORTED, "fft_size=%ld: the HIP FFT covers powers of two 64..4096", N);
+    if (P < 1 || D < P || D % P)
+        return fail(OFDM_ERR_UNSUPPORTED, "num_data_subc=%ld must be a positive multiple of num_pilot_subc=%ld", D,
+                    P);
+    if (P > 256) return fail(OFDM_ERR_UNSUPPORTED, "num_pilot_subc > 256");
+    if (!(k == 1 || k == 2 || k == 4 || k == 6 || k == 8))
+        return fail(OFDM_ERR_INVALID, "modType=%ld is not one of 1,2,4,6,8 (OFDM/modulation.hpp:11-17)", k);
+    if (p->cp_size < 0 || p->cp_size > N) return fail(OFDM_ERR_INVALID, "cp_size out of range");
+    if (p->num_symb < 1 || p->num_pr_symb < 1) return fail(OFDM_ERR_INVALID, "num_symb/num_pr_symb must be >= 1");
+    if ((D * p->num_symb * k) % 8 || (D * k) % 8)
+        return fail(OFDM_ERR_UNSUPPORTED, "num_data_subc*modType must be a multiple of 8 bits");
+    if ((D * p->num_pr_symb) % 8) return fail(OFDM_ERR_UNSUPPORTED, "preamble bits must fill bytes");
+    // layout must stay inside [1, N) without collisions: FFT_FORM ctor Frame.cpp:31-44
+    {
+        std::vector<char> used(N, 0);
+        const long step = D / P + 1, seg = D / P, half = P / 2;
+        long j = 0;
+        auto take = [&](long b) {
+            if (b < 1 || b >= N || used[b]) return false;
+            used[b] = 1;
+            return true;
+        };
+        for (long pos = 1 + seg; j < half; ++j, pos += step) {
+            if (!take(pos)) return fail(OFDM_ERR_INVALID, "pilot comb does not fit fft_size");
+            for (long t = 0; t < seg; ++t)
+                if (!take(pos - seg + t)) return fail(OFDM_ERR_INVALID, "data segments do not fit fft_size");
+        }
+        for (long pos = N - step * half; j < P; ++j, pos += step) {
+            if (!take(pos)) return fail(OFDM_ERR_INVALID, "pilot comb does not fit fft_size");
+            for (long t = 0; t < seg; ++t)
+                if (!take(pos + 1 + t)) return fail(OFDM_ERR_INVALID, "data segments do not fit fft_size");
+        }
+    }
+    if (p->t2sin_size < 0 || (p->t2sin_size && (p->t2_sin_f1 < 0 || p->t2_sin_f1 >= p->t2sin_size ||
+                                                p->t2_sin_f2 < 0 || p->t2_sin_f2 >= p->t2sin_size)))
+        return fail(OFDM_ERR_INVALID, "T2 tones outside T2sin_size");
+    if (p->pr_sin_len < 0 || p->pr_sin_len > (N + p->cp_size) * p->num_pr_symb)
+        return fail(OFDM_ERR_INVALID, "pr_sin_len exceeds the preamble");
+    return OFDM_OK;
+}
+
+int ofdm_destroy(ofdm_ctx* c)
+{
+    if (!c) return OFDM_OK;
+    (void)hipSetDevice(c->device);
+    void* ptrs[] = {c->d_tw, c->d_data_bin, c->d_data_slot, c->d_pilot_bin, c->d_bin_map, c->d_const,
+                    c->d_const_bpsk, c->d_header, c->d_preamble, c->d_templ, c->d_modpre, c->d_t2mask,
+                    c->d_t2tw, c->d_prtw, c->d_scratch};
+    for (void* q : ptrs)
+        if (q) (void)hipFree(q);
+    delete c;
+    return OFDM_OK;
+}
+
+static std::vector<double2> twiddles(int n)
+{
+    std::vector<double2> w(n);
+    for (int j = 0; j < n; ++j) {
+        const double a = 2.0 * M_PI * (double)j / (double)n;
+        w[j] = make_double2(std::cos(a), -std::sin(a));
+    }
+    return w;
+}
+
+// Modulation::Modulation table (modulation.cpp:4-36).
+static std::vector<double2> constellation(int k)
+{
+    std::vector<double2> t(1u << k);
+    if (k == 1) {
+        const double step = M_PI * 2 / (double)2;
+        for (int i = 0; i < 2; ++i) {
+            const cd z = std::exp(cd(0.0, 1.0) * (step * cd(i) + M_PI_4 * 5));
+            t[i] = make_double2(z.real(), z.imag());
+        }
+    } else {
+        const unsigned num = 1u << (k / 2);
+        for (unsigned i = 0; i < t.size(); ++i) {
+            const uint8_t in = (uint8_t)i;
+            t[i] = make_double2(2.0 / (num - 1) * double(in % num) - 1.0, 2.0 / (num - 1) * double(in >> (k / 2)) - 1.0);
+        }
+    }
+    return t;
+}
+
+int ofdm_create(const ofdm_params* params, int device, ofdm_ctx** out)
+{
+    if (!params || !out) return fail(OFDM_ERR_INVALID, "null argument");
+    *out = nullptr;
+    int rc = validate(params);
+    if (rc) return rc;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(OFDM_ERR_HIP, "no HIP device available (the modem core has no CPU path)");
+    if (device < 0 || device >= ndev) return fail(OFDM_ERR_INVALID, "device %d out of range", device);
+    HIP_TRY(hipSetDevice(device));
+
+    ofdm_ctx* c = new ofdm_ctx;
+    c->p = *params;
+    c->device = device;
+    c->N = (int)params->fft_size;
+    c->logn = ilog2_exact(c->N);
+    c->D = (int)params->num_data_subc;
+    c->P = (int)params->num_pilot_subc;
+    c->cp = (int)params->cp_size;
+    c->S = (int)params->num_symb;
+    c->k = (int)params->mod_type;
+    c->L = c->N + c->cp;
+    c->seg = c->D / c->P;
+    c->npr = (int)params->num_pr_symb;
+    c->t2 = (int)params->t2sin_size;
+
+    ofdm_geometry& g = c->geo;
+    g.symbol_len = c->L;
+    g.message_len = (long)c->L * c->S;
+    g.preamble_len = (long)c->L * c->npr;
+    g.frame_len = c->t2 + g.preamble_len + g.message_len;
+    g.ring_len = g.frame_len * (params->rx_buf_size + 1);
+    g.data_per_frame = (long)c->D * c->S;
+    g.bytes_per_frame = (long)c->D * c->S * c->k / 8;
+    g.segment_size = c->seg;
+
+    // FFT_FORM layout (Frame.cpp:31-44)
+    std::vector<int> pilot(c->P), segst(c->P), data_bin(c->D), data_slot(c->D), bin_map(c->N, -1);
+    {
+        const int step = c->seg + 1, half = c->P / 2;
+        int j = 0;
+        for (int pos = 1 + c->seg; j < half; ++j, pos += step) {
+            pilot[j] = pos;
+            segst[j] = pos - c->seg;
+        }
+        for (int pos = c->N - step * half; j < c->P; ++j, pos += step) {
+            pilot[j] = pos;
+            segst[j] = pos + 1;
+        }
+        for (int jj = 0; jj < c->P; ++jj) {
+            g.pilot_bin[jj] = pilot[jj];
+            g.segment_bin[jj] = segst[jj];
+            bin_map[pilot[jj]] = -2;
+            for (int t = 0; t < c->seg; ++t) {
+                const int d = jj * c->seg + t;
+                data_bin[d] = segst[jj] + t;
+                data_slot[d] = jj;
+                bin_map[segst[jj] + t] = d;
+            }
+        }
+    }
+    if ((rc = upload(&c->d_tw, twiddles(c->N))) || (rc = upload(&c->d_data_bin, data_bin)) ||
+        (rc = upload(&c->d_data_slot, data_slot)) || (rc = upload(&c->d_pilot_bin, pilot)) ||
+        (rc = upload(&c->d_bin_map, bin_map)) || (rc = upload(&c->d_const, constellation(c->k))) ||
+        (rc = upload(&c->d_const_bpsk, constellation(1)))) {
+        ofdm_destroy(c);
+        return rc;
+    }
+
+    // T2SIN_FORM::set (Frame.cpp:139-154): X[f1] = X[f2] = 0.5, unnormalised
+    // backward DFT of T2sin_size points = two complex tones of amplitude 0.5.
+    c->t2_symbol.assign(c->t2, cd(0, 0));
+    if (c->t2) {
+        std::vector<cd> spec(c->t2, cd(0, 0));
+        spec[params->t2_sin_f1] = cd(0.5, 0);
+        spec[params->t2_sin_f2] = cd(0.5, 0);
+        for (int n = 0; n < c->t2; ++n) {
+            cd acc(0, 0);
+            for (int kk = 0; kk < c->t2; ++kk) {
+                if (spec[kk] == cd(0, 0)) continue;
+                const double a = 2.0 * M_PI * (double)(((long)kk * n) % c->t2) / (double)c->t2;
+                acc += spec[kk] * cd(std::cos(a), std::sin(a));
+            }
+            c->t2_symbol[n] = acc;
+        }
+    }
+    // T2 detector mask (Frame.cpp:120-133)
+    c->t2_mask.assign(std::max(1, c->t2), 0.0);
+    if (c->t2) {
+        const int sm = (int)params->smooth, f1 = (int)params->t2_sin_f1, f2 = (int)params->t2_sin_f2;
+        for (int i = std::max(0, f1 - sm); i <= std::min(c->t2 - 1, f1 + sm); ++i) c->t2_mask[i] += 1.0;
+        for (int i = std::max(0, f2 - sm); i <= std::min(c->t2 - 1, f2 + sm); ++i) c->t2_mask[i] += 1.0;
+    }
+
+    // PREAMBLE_FORM (Frame.cpp:259-294): mt19937(pr_seed) bytes, BPSK OFDM
+    // symbol(s) made by the tx kernel itself, conj template normalised.
+    {
+        const long nb = (long)c->D * c->npr / 8;
+        c->preamble_bytes.resize(nb);
+        std::mt19937 rng(params->pr_seed);
+        std::uniform_int_distribution<int> dist(0, 255);
+        for (auto& b : c->preamble_bytes) b = (uint8_t)dist(rng);
+
+        const long plen = g.preamble_len;
+        uint8_t* d_b = nullptr;
+        double2* d_pre = nullptr;
+        HIP_TRY(hipMalloc((void**)&d_b, std::max<long>(1, nb)));
+        HIP_TRY(hipMalloc((void**)&d_pre, plen * sizeof(double2)));
+        HIP_TRY(hipMemcpy(d_b, c->preamble_bytes.data(), nb, hipMemcpyHostToDevice));
+        ofdm::TxArgs a{};
+        a.tab = c->tables(true);
+        a.bytes = d_b;
+        a.iq = d_pre;
+        a.nframes = 1;
+        a.frame_stride = plen;
+        a.S = c->npr;
+        a.D = c->D;
+        a.P = c->P;
+        a.cp = c->cp;
+        a.k = 1;
+        a.bytes_per_frame = nb;
+        a.pilot_ampl = (double)params->pilot_ampl / 1000;
+        a.inv_sqrt_n = 1.0 / std::sqrt((double)c->N);
+        a.mult = (double)params->mult;
+        hipError_t e = ofdm::launch_tx(c->logn, a, nullptr);
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+        std::vector<double2> pre(plen);
+        if (e == hipSuccess) e = hipMemcpy(pre.data(), d_pre, plen * sizeof(double2), hipMemcpyDeviceToHost);
+        (void)hipFree(d_b);
+        (void)hipFree(d_pre);
+        if (e != hipSuccess) {
+            ofdm_destroy(c);
+            return hip_fail(e, "preamble synthesis");
+        }
+        c->ofdm_preamble.resize(plen);
+        for (long i = 0; i < plen; ++i) c->ofdm_preamble[i] = cd(pre[i].x, pre[i].y);
+        // mod_preamble = Mod.mod(preamble) (BPSK points, bit_stream_converter(1,8))
+        const auto bp = constellation(1);
+        c->mod_preamble.resize((long)c->D * c->npr);
+        for (long i = 0; i < (long)c->mod_preamble.size(); ++i) {
+            const int bit = (c->preamble_bytes[i >> 3] >> (7 - (i & 7))) & 1;
+            c->mod_preamble[i] = cd(bp[bit].x, bp[bit].y);
+        }
+        const int Lt = (int)params->pr_sin_len;
+        c->templ.resize(Lt);
+        double norm = 0.0;
+        for (int i = 0; i < Lt; ++i) {
+            c->templ[i] = std::conj(c->ofdm_preamble[i]);
+            norm += std::abs(c->templ[i] * c->templ[i]);
+        }
+        norm = std::sqrt(norm);
+        for (int i = 0; i < Lt; ++i) c->templ[i] /= cd(norm);
+    }
+    {
+        std::vector<double2> hdr(c->t2 + g.preamble_len), pre(g.preamble_len), tpl(c->templ.size()),
+            mp(c->mod_preamble.size());
+        for (int i = 0; i < c->t2; ++i) hdr[i] = make_double2(c->t2_symbol[i].real(), c->t2_symbol[i].imag());
+        for (long i = 0; i < g.preamble_len; ++i) {
+            pre[i] = make_double2(c->ofdm_preamble[i].real(), c->ofdm_preamble[i].imag());
+            hdr[c->t2 + i] = pre[i];
+        }
+        for (size_t i = 0; i < tpl.size(); ++i) tpl[i] = make_double2(c->templ[i].real(), c->templ[i].imag());
+        for (size_t i = 0; i < mp.size(); ++i) mp[i] = make_double2(c->mod_preamble[i].real(), c->mod_preamble[i].imag());
+        if ((rc = upload(&c->d_header, hdr)) || (rc = upload(&c->d_preamble, pre)) || (rc = upload(&c->d_templ, tpl)) ||
+            (rc = upload(&c->d_modpre, mp)) || (rc = upload(&c->d_t2mask, c->t2_mask))) {
+            ofdm_destroy(c);
+            return rc;
+        }
+    }
+    *out = c;
+    return OFDM_OK;
+}
+
+int ofdm_get_geometry(const ofdm_ctx* c, ofdm_geometry* o)
+{
+    if (!c || !o) return fail(OFDM_ERR_INVALID, "null argument");
+    *o = c->geo;
+    return OFDM_OK;
+}
+
+int ofdm_get_t2_symbol(const ofdm_ctx* c, double* o)
+{
+    if (!c || !o) return fail(OFDM_ERR_INVALID, "null argument");
+    std::memcpy(o, c->t2_symbol.data(), c->t2_symbol.size() * sizeof(cd));
+    return OFDM_OK;
+}
+
+int ofdm_get_preamble(const ofdm_ctx* c, uint8_t* bytes, double* pre, double* modp, double* templ)
+{
+    if (!c) return fail(OFDM_ERR_INVALID, "null ctx");
+    if (bytes) std::memcpy(bytes, c->preamble_bytes.data(), c->preamble_bytes.size());
+    if (pre) std::memcpy(pre, c->ofdm_preamble.data(), c->ofdm_preamble.size() * sizeof(cd));
+    if (modp) std::memcpy(modp, c->mod_preamble.data(), c->mod_preamble.size() * sizeof(cd));
+    if (templ) std::memcpy(templ, c->templ.data(), c->templ.size() * sizeof(cd));
+    return OFDM_OK;
+}
+
+// ---- memory helpers
+int ofdm_device_alloc(ofdm_ctx* c, size_t bytes, void** d)
+{
+    if (!c || !d) return fail(OFDM_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMalloc(d, std::max<size_t>(bytes, 1)));
+    return OFDM_OK;
+}
+int ofdm_device_free(ofdm_ctx* c, void* d)
+{
+    if (!c) return fail(OFDM_ERR_INVALID, "null ctx");
+    if (d) HIP_TRY(hipFree(d));
+    return OFDM_OK;
+}
+int ofdm_memcpy_h2d(ofdm_ctx* c, void* dst, const void* src, size_t n, void* st)
+{
+    if (!c) return fail(OFDM_ERR_INVALID, "null ctx");
+    HIP_TRY(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, (hipStream_t)st));
+    return OFDM_OK;
+}
+int ofdm_memcpy_d2h(ofdm_ctx* c, void* dst, const void* src, size_t n, void* st)
+{
+    if (!c) return fail(OFDM_ERR_INVALID, "null ctx");
+    HIP_TRY(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, (hipStream_t)st));
+    return OFDM_OK;
+}
+int ofdm_memset_device(ofdm_ctx* c, void* dst, int v, size_t n, void* st)
+{
+    if (!c) return fail(OFDM_ERR_INVALID, "null ctx");
+    HIP_TRY(hipMemsetAsync(dst, v, n, (hipStream_t)st));
+    return OFDM_OK;
+}
+int ofdm_stream_synchronize(ofdm_ctx* c, void* st)
+{
+    if (!c) return fail(OFDM_ERR_INVALID, "null ctx");
+    HIP_TRY(hipStreamSynchronize((hipStream_t)st));
+    return OFDM_OK;
+}
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+static void fill_tx(const ofdm_ctx* c, ofdm::TxArgs& a, const uint8_t* bytes, size_t nframes, double* iq,
+                    size_t stride, int16_t* iq16, const ofdm_channel* ch)
+{
+    a.tab = c->tables(false);
+    a.bytes = bytes;
+    a.iq = reinterpret_cast<double2*>(iq);
+    a.iq16 = iq16;
+    a.nframes = (long)nframes;
+    a.frame_stride = (long)stride;
+    a.S = c->S;
+    a.D = c->D;
+    a.P = c->P;
+    a.cp = c->cp;
+    a.k = c->k;
+    a.bytes_per_frame = c->geo.bytes_per_frame;
+    a.pilot_ampl = (double)c->p.pilot_ampl / 1000;
+    a.inv_sqrt_n = 1.0 / std::sqrt((double)c->N);
+    a.mult = (double)c->p.mult;
+    if (ch && ch->noise_std > 0.0) {
+        a.noise_scale = ch->noise_std * M_SQRT1_2;
+        a.seed = ch->seed;
+        a.sample_offset = ch->sample_offset;
+    }
+}
+
+int ofdm_tx_modulate(ofdm_ctx* c, const uint8_t* bytes, size_t nframes, double* iq_out, size_t frame_stride,
+                     int16_t* iq16_out, const ofdm_channel* ch, void* stream)
+{
+    if (!c || !bytes || !iq_out) return fail(OFDM_ERR_INVALID, "null argument");
+    if (frame_stride < (size_t)c->geo.message_len) return fail(OFDM_ERR_INVALID, "frame_stride < message_len");
+    if (!aligned16(iq_out)) return fail(OFDM_ERR_INVALID, "iq_out must be 16-byte aligned");
+    if (nframes == 0) return OFDM_OK;
+    if (nframes * (size_t)c->S > 0x7fffffffu) return fail(OFDM_ERR_INVALID, "too many symbols in one call");
+    ofdm::TxArgs a{};
+    fill_tx(c, a, bytes, nframes, iq_out, frame_stride, iq16_out, ch);
+    hipError_t e = ofdm::launch_tx(c->logn, a, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "tx_kernel launch");
+    return OFDM_OK;
+}
+
+int ofdm_tx_frames(ofdm_ctx* c, const uint8_t* bytes, size_t nframes, double* frames_out, int16_t* frames16_out,
+                   void* stream)
+{
+    if (!c || !bytes || !frames_out) return fail(OFDM_ERR_INVALID, "null argument");
+    if (!aligned16(frames_out)) return fail(OFDM_ERR_INVALID, "frames_out must be 16-byte aligned");
+    if (nframes == 0) return OFDM_OK;
+    ofdm::TxArgs a{};
+    fill_tx(c, a, bytes, nframes, frames_out, (size_t)c->geo.frame_len, frames16_out, nullptr);
+    a.header = c->d_header;
+    a.header_len = (int)(c->t2 + c->geo.preamble_len);
+    a.msg_offset = a.header_len;
+    hipError_t e = ofdm::launch_tx(c->logn, a, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "tx_kernel launch");
+    return OFDM_OK;
+}
+
+int ofdm_rx_demod(ofdm_ctx* c, const double* iq, size_t nframes, size_t frame_stride, const double* chan,
+                  size_t chan_stride, double* constell_out, uint8_t* bytes_out, const uint8_t* ref_bytes,
+                  unsigned long long* bit_errors, void* stream)
+{
+    if (!c || !iq) return fail(OFDM_ERR_INVALID, "null argument");
+    if (frame_stride < (size_t)c->geo.message_len) return fail(OFDM_ERR_INVALID, "frame_stride < message_len");
+    if (!aligned16(iq) || (chan && !aligned16(chan)) || (constell_out && !aligned16(constell_out)))
+        return fail(OFDM_ERR_INVALID, "complex buffers must be 16-byte aligned");
+    if ((ref_bytes == nullptr) != (bit_errors == nullptr))
+        return fail(OFDM_ERR_INVALID, "ref_bytes and bit_errors go together");
+    if (nframes == 0) return OFDM_OK;
+    if (nframes > 0x7fffffffu) return fail(OFDM_ERR_INVALID, "too many frames in one call");
+    ofdm::RxArgs a{};
+    a.tab = c->tables(false);
+    a.iq = reinterpret_cast<const double2*>(iq);
+    a.nframes = (long)nframes;
+    a.frame_stride = (long)frame_stride;
+    a.chan = reinterpret_cast<const double2*>(chan);
+    a.chan_stride = (long)chan_stride;
+    a.constell = reinterpret_cast<double2*>(constell_out);
+    a.bytes = bytes_out;
+    a.ref = ref_bytes;
+    a.bit_errors = bit_errors;
+    a.S = c->S;
+    a.D = c->D;
+    a.P = c->P;
+    a.seg = c->seg;
+    a.cp = c->cp;
+    a.k = c->k;
+    a.bytes_per_frame = c->geo.bytes_per_frame;
+    a.pilot_ampl = (double)c->p.pilot_ampl / 1000;
+    const bool fits = c->S <= ofdm::RX_SMAX && c->D <= ofdm::RX_DPT * (c->N / 8);
+    if (!fits) {
+        if (c->D > ofdm::RX_DPT * (c->N / 8))
+            return fail(OFDM_ERR_UNSUPPORTED, "num_data_subc > fft_size/2 is not covered by the rx kernel");
+        if (constell_out) {
+            a.ystage = a.constell;
+        } else {
+            const size_t need = nframes * (size_t)c->S * c->D * sizeof(double2);
+            if (need > c->scratch_bytes) {
+                HIP_TRY(hipSetDevice(c->device));
+                if (c->d_scratch) HIP_TRY(hipFree(c->d_scratch));
+                c->d_scratch = nullptr;
+                c->scratch_bytes = 0;
+                HIP_TRY(hipMalloc((void**)&c->d_scratch, need));
+                c->scratch_bytes = need;
+            }
+            a.ystage = c->d_scratch;
+        }
+    }
+    hipError_t e = ofdm::launch_rx(c->logn, a, (hipStream_t)stream, nullptr);
+    if (e != hipSuccess) return hip_fail(e, "rx_kernel launch");
+    return OFDM_OK;
+}
+
+int ofdm_demap(ofdm_ctx* c, double* points, size_t n, uint8_t* bytes_out, void* stream)
+{
+    if (!c || !points || !bytes_out) return fail(OFDM_ERR_INVALID, "null argument");
+    hipError_t e = ofdm::launch_demap(reinterpret_cast<double2*>(points), (long)n, c->k, bytes_out, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "demap launch");
+    return OFDM_OK;
+}
+
+int ofdm_map(ofdm_ctx* c, const uint8_t* bytes, size_t nbytes, double* points_out, void* stream)
+{
+    if (!c || !bytes || !points_out) return fail(OFDM_ERR_INVALID, "null argument");
+    hipError_t e = ofdm::launch_map(bytes, (long)nbytes, c->k, c->d_const, reinterpret_cast<double2*>(points_out),
+                                    (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "map launch");
+    return OFDM_OK;
+}
+
+// ---- sync front end: implemented in ofdm_sync.hip (declared in ofdm_sync.hpp)
+int ofdm_t2_scan(ofdm_ctx* c, const double* iq, size_t n, long start, double* rel_out, int* first_out, void* stream)
+{
+    if (!c || !iq) return fail(OFDM_ERR_INVALID, "null argument");
+    return fail(OFDM_ERR_UNSUPPORTED, "ofdm_t2_scan: not built yet");
+}
+
+int ofdm_find_preamble(ofdm_ctx* c, const double* iq, size_t n, const int* starts, size_t nstarts, int* idx_out,
+                       void* stream)
+{
+    if (!c || !iq) return fail(OFDM_ERR_INVALID, "null argument");
+    return fail(OFDM_ERR_UNSUPPORTED, "ofdm_find_preamble: not built yet");
+}
+
+int ofdm_sync_frames(ofdm_ctx* c, double* frames, size_t nframes, size_t frame_stride, int stages,
+                     const double* cfo_in, double* cfo_out, double* chan_out, void* stream)
+{
+    if (!c || !frames) return fail(OFDM_ERR_INVALID, "null argument");
+    return fail(OFDM_ERR_UNSUPPORTED, "ofdm_sync_frames: not built yet");
+}
+
+}  // extern "C"

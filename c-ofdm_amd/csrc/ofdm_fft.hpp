@@ -1,0 +1,193 @@
+// ofdm_fft.hpp — FP64 complex helpers and the workgroup-wide FFT used by the
+// tx/rx kernels (gfx950 / CDNA4).
+//
+// Replaces the reference's FFTW plans (OFDM/Frame.cpp:16-24 batched
+// forward/backward `fftw_plan_many_dft`, executed at Frame.cpp:64,74): an
+// unnormalised DFT X[k] = sum_n x[n] exp(SIGN*2*pi*i*n*k/N), SIGN = -1
+// (FFTW_FORWARD) or +1 (FFTW_BACKWARD), N = 2^LOGN, 64 <= N <= 4096.
+//
+// Shape: one workgroup of T = N/8 threads per transform. Every pass is a
+// Stockham auto-sort radix-8 pass (last pass radix 2 or 4 when LOGN%3 != 0).
+// Thread t always holds in[t + T*i], i = 0..7, so the first pass reads
+// straight from HBM with 16-B coalesced loads; intermediate passes exchange
+// through LDS (16-B ds_read/ds_write_b128), padded by one 16-B slot every 8
+// elements so the stride-8 writes of the first pass are bank-conflict free.
+// Twiddles come from a per-context table W_N^j (global, L1/L2 resident).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace ofdm {
+
+// ---------------------------------------------------------------- complex
+__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+
+// Complex product. FFT-internal: contraction allowed.
+__device__ __forceinline__ double2 cmul(double2 a, double2 b)
+{
+    return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+
+// Complex product with the exact rounding of g++'s inline _Complex multiply
+// on x86-64 (no FMA): used where the reference's own arithmetic is mirrored.
+__device__ __forceinline__ double2 cmul_exact(double2 a, double2 b)
+{
+    return make_double2(__dsub_rn(__dmul_rn(a.x, b.x), __dmul_rn(a.y, b.y)),
+                        __dadd_rn(__dmul_rn(a.x, b.y), __dmul_rn(a.y, b.x)));
+}
+
+// libgcc __divdc3 (Smith's algorithm) for finite operands — what the
+// reference's std::complex<double> operator/ compiles to.
+__device__ __forceinline__ double2 cdiv_exact(double2 n, double2 d)
+{
+    const double a = n.x, b = n.y, c = d.x, e = d.y;
+    double x, y;
+    if (fabs(c) < fabs(e)) {
+        const double ratio = c / e;
+        const double denom = __dadd_rn(__dmul_rn(c, ratio), e);
+        x = __dadd_rn(__dmul_rn(a, ratio), b) / denom;
+        y = __dsub_rn(__dmul_rn(b, ratio), a) / denom;
+    } else {
+        const double ratio = e / c;
+        const double denom = __dadd_rn(__dmul_rn(e, ratio), c);
+        x = __dadd_rn(__dmul_rn(b, ratio), a) / denom;
+        y = __dsub_rn(b, __dmul_rn(a, ratio)) / denom;
+    }
+    return make_double2(x, y);
+}
+
+// a * (SIGN * i)
+template <int SIGN>
+__device__ __forceinline__ double2 mul_j(double2 a)
+{
+    return SIGN > 0 ? make_double2(-a.y, a.x) : make_double2(a.y, -a.x);
+}
+
+__device__ __forceinline__ int lds_pad(int e) { return e + (e >> 3); }
+
+// ---------------------------------------------------------------- DFTs
+template <int SIGN>
+__device__ __forceinline__ void dft2(double2& a, double2& b)
+{
+    const double2 t = a;
+    a = cadd(t, b);
+    b = csub(t, b);
+}
+
+template <int SIGN>
+__device__ __forceinline__ void dft4(double2& a0, double2& a1, double2& a2, double2& a3)
+{
+    const double2 t0 = cadd(a0, a2), t1 = csub(a0, a2);
+    const double2 t2 = cadd(a1, a3), t3 = mul_j<SIGN>(csub(a1, a3));
+    a0 = cadd(t0, t2);
+    a1 = cadd(t1, t3);
+    a2 = csub(t0, t2);
+    a3 = csub(t1, t3);
+}
+
+template <int SIGN>
+__device__ __forceinline__ void dft8(double2& x0, double2& x1, double2& x2, double2& x3,
+                                     double2& x4, double2& x5, double2& x6, double2& x7)
+{
+    constexpr double C = 0.70710678118654752440084436210484903928483593768847;
+    dft4<SIGN>(x0, x2, x4, x6);  // E0..E3
+    dft4<SIGN>(x1, x3, x5, x7);  // O0..O3
+    // O1 *= W8, O2 *= W8^2 = SIGN*i, O3 *= W8^3
+    const double2 o1 = make_double2((x3.x - SIGN * x3.y) * C, (x3.y + SIGN * x3.x) * C);
+    const double2 o2 = mul_j<SIGN>(x5);
+    const double2 o3 = make_double2(-(x7.x + SIGN * x7.y) * C, (SIGN * x7.x - x7.y) * C);
+    const double2 e0 = x0, e1 = x2, e2 = x4, e3 = x6, o0 = x1;
+    x0 = cadd(e0, o0);
+    x4 = csub(e0, o0);
+    x1 = cadd(e1, o1);
+    x5 = csub(e1, o1);
+    x2 = cadd(e2, o2);
+    x6 = csub(e2, o2);
+    x3 = cadd(e3, o3);
+    x7 = csub(e3, o3);
+}
+
+// ---------------------------------------------------------------- passes
+template <int LOGN>
+struct FftShape {
+    static constexpr int N = 1 << LOGN;
+    static constexpr int T = N / 8;            // threads per transform
+    static constexpr int NPASS8 = LOGN / 3;    // radix-8 passes
+    static constexpr int REM = LOGN % 3;       // trailing radix-2/4 pass
+    static constexpr int LAST_NS = 1 << (3 * NPASS8);
+    static constexpr int PADN = N + N / 8;     // padded LDS elements
+};
+
+// One Stockham pass, radix R, input span Ns. v[i] holds in[t + T*i].
+// Twiddle table tw[j] = exp(-2*pi*i*j/N) (forward); conjugated for SIGN>0.
+template <int LOGN, int R, int NS, int SIGN>
+__device__ __forceinline__ void stockham_pass(double2 (&v)[8], int t, const double2* __restrict__ tw,
+                                              double2* __restrict__ lds)
+{
+    constexpr int N = 1 << LOGN, T = N / 8, B = 8 / R;
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+        const int b = t + T * u;
+        const int k = b & (NS - 1);
+        if constexpr (NS > 1) {
+#pragma unroll
+            for (int r = 1; r < R; ++r) {
+                double2 w = tw[k * r * (N / (NS * R))];
+                if (SIGN > 0) w.y = -w.y;
+                v[u + r * B] = cmul(v[u + r * B], w);
+            }
+        }
+        if constexpr (R == 8)
+            dft8<SIGN>(v[u], v[u + B], v[u + 2 * B], v[u + 3 * B], v[u + 4 * B], v[u + 5 * B],
+                       v[u + 6 * B], v[u + 7 * B]);
+        else if constexpr (R == 4)
+            dft4<SIGN>(v[u], v[u + B], v[u + 2 * B], v[u + 3 * B]);
+        else
+            dft2<SIGN>(v[u], v[u + B]);
+        const int idxD = (b - k) * R + k;
+#pragma unroll
+        for (int r = 0; r < R; ++r) lds[lds_pad(idxD + r * NS)] = v[u + r * B];
+    }
+}
+
+template <int LOGN>
+__device__ __forceinline__ void lds_load8(double2 (&v)[8], int t, const double2* __restrict__ lds)
+{
+    constexpr int T = (1 << LOGN) / 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = lds[lds_pad(t + T * i)];
+}
+
+// Remaining passes after the first one has been written to `lds`.
+template <int LOGN, int PASS, int SIGN>
+__device__ __forceinline__ void fft_tail(double2 (&v)[8], int t, const double2* __restrict__ tw,
+                                         double2* __restrict__ lds)
+{
+    using S = FftShape<LOGN>;
+    constexpr int NPASS = S::NPASS8 + (S::REM ? 1 : 0);
+    if constexpr (PASS < NPASS) {
+        constexpr bool is8 = PASS < S::NPASS8;
+        constexpr int R = is8 ? 8 : (1 << S::REM);
+        constexpr int NS = 1 << (3 * PASS);
+        __syncthreads();  // previous pass fully written
+        lds_load8<LOGN>(v, t, lds);
+        __syncthreads();  // everyone has read before the buffer is overwritten
+        stockham_pass<LOGN, R, NS, SIGN>(v, t, tw, lds);
+        fft_tail<LOGN, PASS + 1, SIGN>(v, t, tw, lds);
+    }
+}
+
+// Full transform. On entry v[i] = x[t + T*i]; on exit the natural-order
+// result X[0..N) is in lds (padded indexing) and the workgroup is synced.
+template <int LOGN, int SIGN>
+__device__ __forceinline__ void fft_block(double2 (&v)[8], int t, const double2* __restrict__ tw,
+                                          double2* __restrict__ lds)
+{
+    using S = FftShape<LOGN>;
+    static_assert(LOGN >= 6 && LOGN <= 12, "N must be 64..4096");
+    stockham_pass<LOGN, 8, 1, SIGN>(v, t, tw, lds);
+    fft_tail<LOGN, 1, SIGN>(v, t, tw, lds);
+    __syncthreads();
+}
+
+}  // namespace ofdm

@@ -1,0 +1,68 @@
+// ofdm_internal.hpp — kernel argument blocks and launcher declarations shared
+// by ofdm_kernels.hip (device code) and ofdm_capi.cpp (the C-ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace ofdm {
+
+// Per-context constant tables, resident in HBM (tiny; L2-resident in practice).
+struct DevTables {
+    const double2* tw;          // N forward twiddles exp(-2*pi*i*j/N)
+    const int* data_bin;        // D: FFT bin of data index d within a symbol
+    const int* data_slot;       // D: pilot slot j = d / seg owning data index d
+    const int* pilot_bin;       // P
+    const int* bin_map;         // N: >=0 data index, -1 unused bin, -2 pilot
+    const double2* constell;    // 2^k mapping table (Modulation::constell)
+};
+
+struct TxArgs {
+    DevTables tab;
+    const uint8_t* bytes;       // nframes * bytes_per_frame
+    double2* iq;                // frame f message at iq + f*frame_stride (+ msg_offset)
+    int16_t* iq16;              // nullable, same indexing, 2 x int16 per sample
+    const double2* header;      // T2+preamble samples (nullable: message only)
+    long nframes;
+    long frame_stride;          // samples
+    long msg_offset;            // samples from frame start to the message
+    int header_len;             // samples of header to copy per frame
+    int S, D, P, cp, k;
+    long bytes_per_frame;
+    double pilot_ampl;
+    double inv_sqrt_n;
+    double mult;
+    // AWGN (noise_std <= 0: off)
+    double noise_scale;         // noise_std / sqrt(2)
+    unsigned long long seed;
+    unsigned long long sample_offset;
+};
+
+struct RxArgs {
+    DevTables tab;
+    const double2* iq;          // frame f message at iq + f*frame_stride
+    long nframes;
+    long frame_stride;
+    const double2* chan;        // nullable: D divisors per frame
+    long chan_stride;           // complex elements between frames (0 = shared)
+    double2* constell;          // nullable
+    uint8_t* bytes;             // nullable
+    const uint8_t* ref;         // nullable
+    unsigned long long* bit_errors;  // nullable
+    double2* ystage;            // staged variant only: nframes*S*D scratch
+    int S, D, P, seg, cp, k;
+    long bytes_per_frame;
+    double pilot_ampl;
+};
+
+// Launchers (ofdm_kernels.hip). Return hipSuccess or the launch error.
+hipError_t launch_tx(int logn, const TxArgs& a, hipStream_t stream);
+hipError_t launch_rx(int logn, const RxArgs& a, hipStream_t stream, bool* staged_needed);
+hipError_t launch_demap(double2* pts, long n, int k, uint8_t* bytes, hipStream_t stream);
+hipError_t launch_map(const uint8_t* bytes, long nbytes, int k, const double2* table, double2* out,
+                      hipStream_t stream);
+
+// Register-resident rx limits: S*ceil(D/T) <= RX_REG_SLOTS.
+constexpr int RX_SMAX = 8;
+constexpr int RX_DPT = 4;
+
+}  // namespace ofdm

@@ -1,0 +1,468 @@
+// ofdm_kernels.hip — hand-written HIP kernels for the OFDM modem hot path on
+// MI355X (gfx950). FP64 throughout (the reference computes in
+// std::complex<double>); memory-bound by design (~2.4 flop/B),
+// so no MFMA: the levers are coalesced 16-B HBM traffic, LDS-resident FFT
+// passes and one HBM round trip per sample.
+//
+//   tx_kernel   : Modulation::mod (modulation.cpp:39-50) + FFT_FORM::write
+//                 (Frame.cpp:54-70) + OFDM_FORM::write CP attach
+//                 (Frame.cpp:185-198) [+ FRAME_FORM::get_int16, Frame.cpp:249-256]
+//                 — one workgroup per OFDM symbol.
+//   rx_kernel   : OFDM_FORM::fft CP strip (Frame.hpp:276-282) + FFT_FORM::read
+//                 (Frame.cpp:73-96) [+ caller's chan divide, main.cpp:69-71]
+//                 + Modulation::demod (modulation.cpp:53-87) + bit-error count
+//                 — one workgroup per frame; the frame's data carriers stay in
+//                 VGPRs until the frame-global pilot normalisation is known.
+//   demap/map   : Modulation::demod / ::mod on flat point arrays.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "ofdm_fft.hpp"
+#include "ofdm_internal.hpp"
+
+namespace ofdm {
+
+// ------------------------------------------------------------------ helpers
+
+// k-bit symbol g of an MSB-first byte stream (bit_stream_converter(k, 8, ...),
+// modulation.cpp:90-125; bits past the end read as the converter's zero pad).
+__device__ __forceinline__ int symbol_bits(const uint8_t* __restrict__ b, long nbytes, long g, int k)
+{
+    const long bit = g * k;
+    const long byte = bit >> 3;
+    const int off = (int)(bit & 7);
+    const int mask = (1 << k) - 1;
+    if (off + k <= 8) return (b[byte] >> (8 - off - k)) & mask;
+    const int w = ((int)b[byte] << 8) | (byte + 1 < nbytes ? (int)b[byte + 1] : 0);
+    return (w >> (16 - off - k)) & mask;
+}
+
+// Modulation::demod decision for one point (modulation.cpp:62-84): BPSK
+// re+im > 0; QAM clamp to [-1,1] then uint8((v+1)*str_size_1 + 0.5) per axis,
+// idx = re | im*str_size. Separate roundings (no FMA) as on x86-64.
+__device__ __forceinline__ int decide(double2 z, int k, double s1, int m)
+{
+    if (k == 1) return (z.x + z.y) > 0.0;
+    const double re = z.x < -1.0 ? -1.0 : (1.0 < z.x ? 1.0 : z.x);
+    const double im = z.y < -1.0 ? -1.0 : (1.0 < z.y ? 1.0 : z.y);
+    const int ire = (uint8_t)(int)__dadd_rn(__dmul_rn(__dadd_rn(re, 1.0), s1), 0.5);
+    const int iim = (uint8_t)(int)__dadd_rn(__dmul_rn(__dadd_rn(im, 1.0), s1), 0.5);
+    return (ire | (iim * m)) & 0xff;
+}
+
+__device__ __forceinline__ double2 clamp_point(double2 z)
+{
+    return make_double2(z.x < -1.0 ? -1.0 : (1.0 < z.x ? 1.0 : z.x),
+                        z.y < -1.0 ? -1.0 : (1.0 < z.y ? 1.0 : z.y));
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z)
+{
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// Counter-based Box-Muller AWGN (same definition as oracle orc_awgn).
+__device__ __forceinline__ double2 awgn_sample(unsigned long long seed, unsigned long long g, double sc)
+{
+    const uint64_t h1 = mix64(seed + 0x9E3779B97F4A7C15ull * (2 * g + 1));
+    const uint64_t h2 = mix64(seed + 0x9E3779B97F4A7C15ull * (2 * g + 2));
+    const double u1 = (double)((h1 >> 11) + 1) * 0x1.0p-53;
+    const double u2 = (double)(h2 >> 11) * 0x1.0p-53;
+    const double r = sqrt(-2.0 * log(u1)) * sc;
+    double sn, cs;
+    sincos(2.0 * M_PI * u2, &sn, &cs);
+    return make_double2(r * cs, r * sn);
+}
+
+__device__ __forceinline__ int16_t to_int16(double v) { return (int16_t)(int)v; }
+
+template <int NT>
+__device__ __forceinline__ double block_sum(double v, double* red)
+{
+#pragma unroll
+    for (int o = (NT >= 64 ? 32 : NT / 2); o > 0; o >>= 1) v += __shfl_xor(v, o);
+    constexpr int NW = (NT + 63) / 64;
+    if constexpr (NW == 1) {
+        return v;
+    } else {
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        __syncthreads();
+        if (lane == 0) red[w] = v;
+        __syncthreads();
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) s += red[i];
+        return s;
+    }
+}
+
+template <int NT>
+__device__ __forceinline__ unsigned long long block_sum_u64(unsigned long long v, double* red)
+{
+    for (int o = (NT >= 64 ? 32 : NT / 2); o > 0; o >>= 1) v += __shfl_xor(v, o);
+    constexpr int NW = (NT + 63) / 64;
+    if constexpr (NW == 1) {
+        return v;
+    } else {
+        unsigned long long* r = reinterpret_cast<unsigned long long*>(red);
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        __syncthreads();
+        if (lane == 0) r[w] = v;
+        __syncthreads();
+        unsigned long long s = 0;
+        for (int i = 0; i < NW; ++i) s += r[i];
+        return s;
+    }
+}
+
+// ------------------------------------------------------------------ tx
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 8) tx_kernel(TxArgs a)
+{
+    using FS = FftShape<LOGN>;
+    constexpr int N = FS::N, T = FS::T;
+    extern __shared__ double2 smem[];
+    const int t = threadIdx.x;
+    const long sym = blockIdx.x;
+    const long f = sym / a.S;
+    const int s = (int)(sym - f * a.S);
+    const uint8_t* fb = a.bytes + f * a.bytes_per_frame;
+
+    // FFT_FORM::write: zero, pilots = pilot_ampl, segments <- mapped points.
+    double2 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int m = a.tab.bin_map[t + T * i];
+        if (m >= 0) {
+            const int val = symbol_bits(fb, a.bytes_per_frame, (long)s * a.D + m, a.k);
+            v[i] = a.tab.constell[val];
+        } else {
+            v[i] = make_double2(m == -2 ? a.pilot_ampl : 0.0, 0.0);
+        }
+    }
+    fft_block<LOGN, +1>(v, t, a.tab.tw, smem);
+
+    // body / sqrt(N) after a CP copy of its last cp samples (Frame.cpp:66-68,191-197)
+    const int L = N + a.cp;
+    const long base = f * a.frame_stride + a.msg_offset + (long)s * L;
+    double2* out = a.iq + base;
+    int16_t* out16 = a.iq16 ? a.iq16 + 2 * base : nullptr;
+    const unsigned long long g0 = a.sample_offset + (unsigned long long)(f * (long)a.S + s) * L;
+    for (int j = t; j < L; j += T) {
+        const int n = j < a.cp ? N - a.cp + j : j - a.cp;
+        double2 z = smem[lds_pad(n)];
+        z.x *= a.inv_sqrt_n;
+        z.y *= a.inv_sqrt_n;
+        if (out16) {
+            out16[2 * j] = to_int16(z.x * a.mult);
+            out16[2 * j + 1] = to_int16(z.y * a.mult);
+        }
+        if (a.noise_scale > 0.0) {
+            const double2 w = awgn_sample(a.seed, g0 + j, a.noise_scale);
+            z.x += w.x;
+            z.y += w.y;
+        }
+        out[j] = z;
+    }
+    // [T2 | preamble] header of full FRAME_FORM buffers (Frame.cpp:219,228-229)
+    if (a.header && s == 0) {
+        double2* fr = a.iq + f * a.frame_stride;
+        int16_t* fr16 = a.iq16 ? a.iq16 + 2 * f * a.frame_stride : nullptr;
+        for (int j = t; j < a.header_len; j += T) {
+            const double2 z = a.header[j];
+            fr[j] = z;
+            if (fr16) {
+                fr16[2 * j] = to_int16(z.x * a.mult);
+                fr16[2 * j + 1] = to_int16(z.y * a.mult);
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------ rx
+// STAGED=false: the frame's S*D equalisation inputs live in VGPRs
+//   (S <= RX_SMAX, D <= RX_DPT*T). A rolled symbol loop shifts them through a
+//   fixed register window so every register index stays compile-time.
+// STAGED=true: any S; inputs parked in a_.ystage (same-thread re-read).
+template <int LOGN, bool STAGED>
+__global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
+{
+    using FS = FftShape<LOGN>;
+    constexpr int N = FS::N, T = FS::T;
+    constexpr int SW = STAGED ? 1 : RX_SMAX;  // register window (symbols)
+    extern __shared__ double2 smem[];
+    const int S = a.S, D = a.D, P = a.P;
+    double2* lds = smem;
+    double2* pil = smem + FS::PADN;       // S*P raw pilots
+    double2* gain = pil + S * P;          // S*P equaliser gains
+    double* red = reinterpret_cast<double*>(gain + S * P);
+    uint8_t* dec = reinterpret_cast<uint8_t*>(smem);  // aliases lds after the FFTs
+
+    const int t = threadIdx.x;
+    const long f = blockIdx.x;
+    const int L = N + a.cp;
+    const double2* x = a.iq + f * a.frame_stride;
+
+    int bins[RX_DPT], slot[RX_DPT];
+#pragma unroll
+    for (int i = 0; i < RX_DPT; ++i) {
+        const int d = t + T * i;
+        bins[i] = d < D ? a.tab.data_bin[d] : 0;
+        slot[i] = d < D ? a.tab.data_slot[d] : 0;
+    }
+
+    double2 y[SW][RX_DPT];
+#pragma unroll 1
+    for (int s = 0; s < S; ++s) {
+        const double2* sym = x + (long)s * L + a.cp;  // CP strip
+        double2 v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = sym[t + T * i];
+        fft_block<LOGN, -1>(v, t, a.tab.tw, lds);
+        for (int j = t; j < P; j += T) pil[s * P + j] = lds[lds_pad(a.tab.pilot_bin[j])];
+        if constexpr (STAGED) {
+#pragma unroll
+            for (int i = 0; i < RX_DPT; ++i) {
+                const int d = t + T * i;
+                if (d < D) a.ystage[(f * S + s) * D + d] = lds[lds_pad(bins[i])];
+            }
+        } else {
+#pragma unroll
+            for (int w = 0; w < SW - 1; ++w)
+#pragma unroll
+                for (int i = 0; i < RX_DPT; ++i) y[w][i] = y[w + 1][i];
+#pragma unroll
+            for (int i = 0; i < RX_DPT; ++i) y[SW - 1][i] = lds[lds_pad(bins[i])];
+        }
+        __syncthreads();  // lds reused by the next symbol
+    }
+
+    // phys_pilot_ampl = sum |pilot| / (P*S*pilot_ampl)   (Frame.cpp:76-80)
+    double acc = 0.0;
+    for (int i = t; i < S * P; i += T) acc += hypot(pil[i].x, pil[i].y);
+    acc = block_sum<T>(acc, red);
+    const double phys = acc / ((double)(P * S) * a.pilot_ampl);
+
+    // out = (F/phys) / ((F[s,p]/phys) / (F[0,p]/phys)) = F * gain[s][j]   (Frame.cpp:82-93)
+    for (int i = t; i < S * P; i += T) {
+        const int j = i % P;
+        const double2 c0 = make_double2(pil[j].x / phys, pil[j].y / phys);
+        const double2 cs = make_double2(pil[i].x / phys, pil[i].y / phys);
+        const double2 coef = cdiv_exact(cs, c0);
+        const double2 g = cdiv_exact(make_double2(1.0, 0.0), coef);
+        gain[i] = make_double2(g.x / phys, g.y / phys);
+    }
+    __syncthreads();
+
+    const int m = 1 << (a.k / 2);
+    const double s1 = a.k == 1 ? 0.0 : 1.0 / (2.0 / (m - 1));
+    const double2* chan = a.chan ? a.chan + f * a.chan_stride : nullptr;
+    const bool whole_frame_dec = (long)S * D <= (long)FS::PADN * 16;
+
+    auto emit = [&](int s, int i, double2 yv) {
+        const int d = t + T * i;
+        double2 o = cmul_exact(yv, gain[s * P + slot[i]]);
+        if (chan) o = cdiv_exact(o, chan[d]);
+        if (a.constell) a.constell[(f * S + s) * D + d] = o;
+        dec[whole_frame_dec ? s * D + d : d] = (uint8_t)decide(o, a.k, s1, m);
+    };
+
+    const long bpf = a.bytes_per_frame;
+    unsigned long long errs = 0;
+    auto pack = [&](long jb0, long jb1, long dbase) {
+        for (long jb = jb0 + t; jb < jb1; jb += T) {
+            int byte = 0;
+            if (a.k == 1 || a.k == 2 || a.k == 4 || a.k == 8) {
+                const int per = 8 / a.k;
+                const long p0 = (jb - jb0) * per + dbase;
+                for (int r = 0; r < per; ++r) byte = (byte << a.k) | dec[p0 + r];
+            } else {
+                for (int b = 0; b < 8; ++b) {
+                    const long bit = (jb - jb0) * 8 + b;
+                    const long g = bit / a.k + dbase;
+                    const int within = (int)(bit % a.k);
+                    byte = (byte << 1) | ((dec[g] >> (a.k - 1 - within)) & 1);
+                }
+            }
+            if (a.bytes) a.bytes[f * bpf + jb] = (uint8_t)byte;
+            if (a.ref) errs += __popc((unsigned)(byte ^ a.ref[f * bpf + jb]));
+        }
+    };
+
+    if constexpr (!STAGED) {
+#pragma unroll
+        for (int w = 0; w < SW; ++w) {
+            const int s = w - (SW - S);
+            if (s >= 0) {
+#pragma unroll
+                for (int i = 0; i < RX_DPT; ++i)
+                    if (t + T * i < D) emit(s, i, y[w][i]);
+            }
+        }
+        __syncthreads();
+        pack(0, bpf, 0);
+    } else {
+        const long bps = (long)D * a.k / 8;  // bytes per symbol (host checks D*k % 8 == 0)
+        for (int s = 0; s < S; ++s) {
+#pragma unroll
+            for (int i = 0; i < RX_DPT; ++i)
+                if (t + T * i < D) emit(s, i, a.ystage[(f * S + s) * D + t + T * i]);
+            __syncthreads();
+            if (whole_frame_dec)
+                ;  // packed once below
+            else {
+                pack(s * bps, (s + 1) * bps, 0);
+                __syncthreads();
+            }
+        }
+        if (whole_frame_dec) {
+            __syncthreads();
+            pack(0, bpf, 0);
+        }
+    }
+    if (a.bit_errors) {
+        errs = block_sum_u64<T>(errs, red);
+        if (t == 0 && errs) atomicAdd(a.bit_errors, errs);
+    }
+}
+
+// ------------------------------------------------------------------ demap / map
+// Modulation::demod on n points: one thread per output byte.
+__global__ void demap_kernel(double2* pts, long n, int k, uint8_t* bytes, long nbytes)
+{
+    const long jb = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (jb >= nbytes) return;
+    const int m = 1 << (k / 2);
+    const double s1 = k == 1 ? 0.0 : 1.0 / (2.0 / (m - 1));
+    const long g0 = (jb * 8) / k, g1 = (jb * 8 + 7) / k;
+    int dv[9];
+    for (long g = g0; g <= g1; ++g) {
+        int dcs = 0;
+        if (g < n) {
+            const double2 z = pts[g];
+            dcs = decide(z, k, s1, m);
+            if (k != 1 && (g * k) / 8 == jb) pts[g] = clamp_point(z);
+        }
+        dv[g - g0] = dcs;
+    }
+    int byte = 0;
+    for (int b = 0; b < 8; ++b) {
+        const long bit = jb * 8 + b;
+        const long g = bit / k;
+        const int within = (int)(bit % k);
+        const int bitv = g < n ? (dv[g - g0] >> (k - 1 - within)) & 1 : 0;
+        byte = (byte << 1) | bitv;
+    }
+    bytes[jb] = (uint8_t)byte;
+}
+
+__global__ void map_kernel(const uint8_t* bytes, long nbytes, int k, const double2* table, double2* out,
+                           long npts)
+{
+    const long g = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (g >= npts) return;
+    out[g] = table[symbol_bits(bytes, nbytes, g, k)];
+}
+
+// ------------------------------------------------------------------ launchers
+template <int LOGN>
+static hipError_t tx_launch_n(const TxArgs& a, hipStream_t st)
+{
+    using FS = FftShape<LOGN>;
+    const size_t shm = sizeof(double2) * FS::PADN;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)tx_kernel<LOGN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+        attr = true;
+    }
+    const long grid = a.nframes * a.S;
+    if (grid <= 0) return hipSuccess;
+    hipLaunchKernelGGL(tx_kernel<LOGN>, dim3((unsigned)grid), dim3(FS::T), shm, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_tx(int logn, const TxArgs& a, hipStream_t st)
+{
+    switch (logn) {
+        case 6: return tx_launch_n<6>(a, st);
+        case 7: return tx_launch_n<7>(a, st);
+        case 8: return tx_launch_n<8>(a, st);
+        case 9: return tx_launch_n<9>(a, st);
+        case 10: return tx_launch_n<10>(a, st);
+        case 11: return tx_launch_n<11>(a, st);
+        case 12: return tx_launch_n<12>(a, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <int LOGN>
+static size_t rx_shm(const RxArgs& a)
+{
+    using FS = FftShape<LOGN>;
+    return sizeof(double2) * (FS::PADN + 2 * (size_t)a.S * a.P) + 32 * sizeof(double);
+}
+
+template <int LOGN, bool STAGED>
+static hipError_t rx_launch_n(const RxArgs& a, hipStream_t st)
+{
+    using FS = FftShape<LOGN>;
+    const size_t shm = rx_shm<LOGN>(a);
+    if (shm > 160 * 1024) return hipErrorInvalidValue;
+    static int attr = 0;
+    if ((size_t)attr < shm) {
+        (void)hipFuncSetAttribute((const void*)rx_kernel<LOGN, STAGED>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024);
+        attr = 160 * 1024;
+    }
+    if (a.nframes <= 0) return hipSuccess;
+    hipLaunchKernelGGL((rx_kernel<LOGN, STAGED>), dim3((unsigned)a.nframes), dim3(FS::T), shm, st, a);
+    return hipGetLastError();
+}
+
+template <int LOGN>
+static hipError_t rx_dispatch(const RxArgs& a, hipStream_t st, bool* staged)
+{
+    using FS = FftShape<LOGN>;
+    const bool fits = a.S <= RX_SMAX && a.D <= RX_DPT * FS::T;
+    if (staged) *staged = !fits;
+    if (!fits && a.ystage == nullptr) return hipErrorInvalidValue;
+    return fits ? rx_launch_n<LOGN, false>(a, st) : rx_launch_n<LOGN, true>(a, st);
+}
+
+hipError_t launch_rx(int logn, const RxArgs& a, hipStream_t st, bool* staged)
+{
+    switch (logn) {
+        case 6: return rx_dispatch<6>(a, st, staged);
+        case 7: return rx_dispatch<7>(a, st, staged);
+        case 8: return rx_dispatch<8>(a, st, staged);
+        case 9: return rx_dispatch<9>(a, st, staged);
+        case 10: return rx_dispatch<10>(a, st, staged);
+        case 11: return rx_dispatch<11>(a, st, staged);
+        case 12: return rx_dispatch<12>(a, st, staged);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_demap(double2* pts, long n, int k, uint8_t* bytes, hipStream_t st)
+{
+    const long nbytes = (n * k + 7) / 8;
+    if (nbytes <= 0) return hipSuccess;
+    const int bs = 256;
+    hipLaunchKernelGGL(demap_kernel, dim3((unsigned)((nbytes + bs - 1) / bs)), dim3(bs), 0, st, pts, n, k, bytes,
+                       nbytes);
+    return hipGetLastError();
+}
+
+hipError_t launch_map(const uint8_t* bytes, long nbytes, int k, const double2* table, double2* out, hipStream_t st)
+{
+    const long npts = (nbytes * 8 + k - 1) / k;
+    if (npts <= 0) return hipSuccess;
+    const int bs = 256;
+    hipLaunchKernelGGL(map_kernel, dim3((unsigned)((npts + bs - 1) / bs)), dim3(bs), 0, st, bytes, nbytes, k, table,
+                       out, npts);
+    return hipGetLastError();
+}
+
+}  // namespace ofdm

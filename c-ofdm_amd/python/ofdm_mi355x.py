@@ -1,0 +1,233 @@
+"""ofdm_mi355x — Python view of the C-ABI in include/ofdm_mi355x.h.
+
+Thin ctypes binding over c-ofdm_amd/lib/libofdm_mi355x.so for tests and
+bench.py. Device buffers are torch tensors on cuda (PyTorch is plumbing here:
+HBM allocation, streams, events, torch.distributed); every compute call goes
+through the HIP kernels of the shared library. There is no CPU fallback: if
+the library is missing, import of `lib()` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+LIB_PATH = os.path.join(PKG, "lib", "libofdm_mi355x.so")
+HEADER = os.path.join(os.path.dirname(PKG), "include", "ofdm_mi355x.h")
+
+PARAM_FIELDS = [
+    "fft_size", "num_data_subc", "num_pilot_subc", "cp_size", "num_symb", "num_pr_symb",
+    "pr_sin_len", "pr_seed", "pr_level", "t2sin_size", "t2_sin_f1", "t2_sin_f2",
+    "t2_sin_level", "smooth", "mod_type", "pilot_ampl", "mult", "rx_buf_size", "iterations",
+]
+
+OFDM_OK = 0
+ERRORS = {-1: "INVALID", -2: "UNSUPPORTED", -3: "HIP", -4: "IO", -5: "NOMEM", -6: "PARSE"}
+SYNC_CFO, SYNC_FREQ_SHIFT, SYNC_CP, SYNC_PHASE, SYNC_CHAN, SYNC_ALL = 1, 2, 4, 8, 16, 31
+
+
+class Params(C.Structure):
+    _fields_ = [(f, C.c_long) for f in PARAM_FIELDS]
+
+    @classmethod
+    def make(cls, **kw) -> "Params":
+        p = cls()
+        for f in PARAM_FIELDS:
+            setattr(p, f, int(kw.get(f, 0)))
+        return p
+
+    def as_dict(self) -> dict:
+        return {f: getattr(self, f) for f in PARAM_FIELDS}
+
+
+class Geometry(C.Structure):
+    _fields_ = [("symbol_len", C.c_long), ("message_len", C.c_long), ("preamble_len", C.c_long),
+                ("frame_len", C.c_long), ("ring_len", C.c_long), ("data_per_frame", C.c_long),
+                ("bytes_per_frame", C.c_long), ("segment_size", C.c_long),
+                ("pilot_bin", C.c_long * 256), ("segment_bin", C.c_long * 256)]
+
+
+class Channel(C.Structure):
+    _fields_ = [("noise_std", C.c_double), ("seed", C.c_ulonglong), ("sample_offset", C.c_ulonglong)]
+
+
+class OfdmError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"ofdm error {code} ({ERRORS.get(code, '?')}): {msg}")
+        self.code = code
+
+
+# Every symbol include/ofdm_mi355x.h declares, with its ctypes signature.
+_V, _I, _L, _SZ, _D = C.c_void_p, C.c_int, C.c_long, C.c_size_t, C.c_double
+_PP = C.POINTER(Params)
+SIGNATURES = {
+    "ofdm_last_error": (C.c_char_p, []),
+    "ofdm_abi_version": (_I, []),
+    "ofdm_params_default": (_I, [_PP]),
+    "ofdm_params_from_config": (_I, [C.c_char_p, _PP]),
+    "ofdm_config_lookup": (_I, [C.c_char_p, C.c_char_p, C.POINTER(C.c_long)]),
+    "ofdm_create": (_I, [_PP, _I, C.POINTER(_V)]),
+    "ofdm_destroy": (_I, [_V]),
+    "ofdm_get_geometry": (_I, [_V, C.POINTER(Geometry)]),
+    "ofdm_get_t2_symbol": (_I, [_V, _V]),
+    "ofdm_get_preamble": (_I, [_V, _V, _V, _V, _V]),
+    "ofdm_device_alloc": (_I, [_V, _SZ, C.POINTER(_V)]),
+    "ofdm_device_free": (_I, [_V, _V]),
+    "ofdm_memcpy_h2d": (_I, [_V, _V, _V, _SZ, _V]),
+    "ofdm_memcpy_d2h": (_I, [_V, _V, _V, _SZ, _V]),
+    "ofdm_memset_device": (_I, [_V, _V, _I, _SZ, _V]),
+    "ofdm_stream_synchronize": (_I, [_V, _V]),
+    "ofdm_tx_modulate": (_I, [_V, _V, _SZ, _V, _SZ, _V, C.POINTER(Channel), _V]),
+    "ofdm_tx_frames": (_I, [_V, _V, _SZ, _V, _V, _V]),
+    "ofdm_rx_demod": (_I, [_V, _V, _SZ, _SZ, _V, _SZ, _V, _V, _V, _V, _V]),
+    "ofdm_demap": (_I, [_V, _V, _SZ, _V, _V]),
+    "ofdm_map": (_I, [_V, _V, _SZ, _V, _V]),
+    "ofdm_t2_scan": (_I, [_V, _V, _SZ, _L, _V, _V, _V]),
+    "ofdm_find_preamble": (_I, [_V, _V, _SZ, _V, _SZ, _V, _V]),
+    "ofdm_sync_frames": (_I, [_V, _V, _SZ, _SZ, _I, _V, _V, _V, _V]),
+}
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", PKG, "-j8"], check=True)
+
+
+def lib():
+    """Load the HIP shared library (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError(f"{LIB_PATH} missing: run `make -C c-ofdm_amd` (no CPU fallback exists)")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != OFDM_OK:
+        raise OfdmError(rc, lib().ofdm_last_error().decode())
+
+
+def params_default() -> Params:
+    p = Params()
+    check(lib().ofdm_params_default(C.byref(p)))
+    return p
+
+
+def params_from_config(path: str) -> Params:
+    p = Params()
+    check(lib().ofdm_params_from_config(path.encode(), C.byref(p)))
+    return p
+
+
+def config_lookup(path: str, key: str) -> int:
+    v = C.c_long()
+    check(lib().ofdm_config_lookup(path.encode(), key.encode(), C.byref(v)))
+    return v.value
+
+
+def _ptr(t):
+    """Device (or host numpy) pointer of a tensor/array, or None."""
+    if t is None:
+        return None
+    if hasattr(t, "data_ptr"):
+        return t.data_ptr()
+    return t.ctypes.data
+
+
+def _stream(stream):
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    return stream if isinstance(stream, int) else stream.cuda_stream
+
+
+class Modem:
+    """One ofdm_ctx: the FRAME_FORM constants for a config on one GPU."""
+
+    def __init__(self, params, device: int = 0):
+        if isinstance(params, dict):
+            params = Params.make(**params)
+        self.params = params
+        self.device = device
+        h = C.c_void_p()
+        check(lib().ofdm_create(C.byref(params), device, C.byref(h)))
+        self.h = h
+        g = Geometry()
+        check(lib().ofdm_get_geometry(h, C.byref(g)))
+        self.geo = g
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().ofdm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- constants
+    def t2_symbol(self):
+        import numpy as np
+        out = np.zeros(self.params.t2sin_size, np.complex128)
+        check(lib().ofdm_get_t2_symbol(self.h, out.ctypes.data))
+        return out
+
+    def preamble(self):
+        import numpy as np
+        p = self.params
+        b = np.zeros(p.num_data_subc * p.num_pr_symb // 8, np.uint8)
+        pre = np.zeros(self.geo.preamble_len, np.complex128)
+        modp = np.zeros(p.num_data_subc * p.num_pr_symb, np.complex128)
+        tpl = np.zeros(p.pr_sin_len, np.complex128)
+        check(lib().ofdm_get_preamble(self.h, b.ctypes.data, pre.ctypes.data, modp.ctypes.data,
+                                      tpl.ctypes.data))
+        return b, pre, modp, tpl
+
+    # ---- compute (device tensors)
+    def tx(self, data, nframes: int, iq_out, frame_stride: int | None = None, iq16_out=None,
+           noise_std: float = 0.0, seed: int = 0, sample_offset: int = 0, stream=None):
+        stride = self.geo.message_len if frame_stride is None else frame_stride
+        ch = Channel(noise_std, seed, sample_offset) if noise_std > 0 else None
+        check(lib().ofdm_tx_modulate(self.h, _ptr(data), nframes, _ptr(iq_out), stride,
+                                     _ptr(iq16_out), C.byref(ch) if ch else None, _stream(stream)))
+
+    def tx_frames(self, data, nframes: int, frames_out, frames16_out=None, stream=None):
+        check(lib().ofdm_tx_frames(self.h, _ptr(data), nframes, _ptr(frames_out), _ptr(frames16_out),
+                                   _stream(stream)))
+
+    def rx(self, iq, nframes: int, frame_stride: int | None = None, chan=None, chan_stride: int = 0,
+           constell_out=None, bytes_out=None, ref=None, bit_errors=None, stream=None):
+        stride = self.geo.message_len if frame_stride is None else frame_stride
+        check(lib().ofdm_rx_demod(self.h, _ptr(iq), nframes, stride, _ptr(chan), chan_stride,
+                                  _ptr(constell_out), _ptr(bytes_out), _ptr(ref), _ptr(bit_errors),
+                                  _stream(stream)))
+
+    def demap(self, points, n: int, bytes_out, stream=None):
+        check(lib().ofdm_demap(self.h, _ptr(points), n, _ptr(bytes_out), _stream(stream)))
+
+    def map(self, data, nbytes: int, points_out, stream=None):
+        check(lib().ofdm_map(self.h, _ptr(data), nbytes, _ptr(points_out), _stream(stream)))
+
+    def t2_scan(self, iq, n: int, start: int, rel_out=None, first_out=None, stream=None):
+        check(lib().ofdm_t2_scan(self.h, _ptr(iq), n, start, _ptr(rel_out), _ptr(first_out),
+                                 _stream(stream)))
+
+    def find_preamble(self, iq, n: int, starts, nstarts: int, idx_out, stream=None):
+        check(lib().ofdm_find_preamble(self.h, _ptr(iq), n, _ptr(starts), nstarts, _ptr(idx_out),
+                                       _stream(stream)))
+
+    def sync_frames(self, frames, nframes: int, frame_stride: int, stages: int = SYNC_ALL,
+                    cfo_in=None, cfo_out=None, chan_out=None, stream=None):
+        check(lib().ofdm_sync_frames(self.h, _ptr(frames), nframes, frame_stride, stages, _ptr(cfo_in),
+                                     _ptr(cfo_out), _ptr(chan_out), _stream(stream)))

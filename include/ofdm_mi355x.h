@@ -12,7 +12,7 @@
  *   - Every function returns an int status: OFDM_OK (0) or a negative
  *     OFDM_ERR_* code; ofdm_last_error() gives a thread-local message.
  *   - Complex samples are interleaved FP64 {re, im} (the std::complex<double>
- *     layout of the reference and of its data/*.bin files).
+ *     layout of the reference and of its data/<name>.bin files).
  *   - Batched compute entry points take DEVICE pointers and an explicit HIP
  *     stream passed as void* (NULL = the legacy default stream). They are
  *     asynchronous; they never allocate, copy to the host or synchronise, so

@@ -1,0 +1,65 @@
+"""Shared test helpers: golden fixtures, configs, seeded payloads."""
+import json
+import os
+
+import numpy as np
+
+import oracle as O
+
+GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def golden():
+    with open(os.path.join(GOLDEN_DIR, "golden.json")) as f:
+        meta = json.load(f)
+    g = dict(meta)
+    g["source"] = np.load(os.path.join(GOLDEN_DIR, "source_bin.npy"))
+    d = np.load(os.path.join(GOLDEN_DIR, "data_bin_i16.npz"))["iq"].astype(np.float64)
+    g["data"] = d[0::2] + 1j * d[1::2]
+    g["t2_corr"] = np.load(os.path.join(GOLDEN_DIR, "t2_sin_corr.npy"))
+    g["phases"] = np.load(os.path.join(GOLDEN_DIR, "phases.npy"))
+    g["constell"] = np.load(os.path.join(GOLDEN_DIR, "constell.npy"))
+    with open(os.path.join(GOLDEN_DIR, "data_txt.bin"), "rb") as f:
+        g["payload_text"] = np.frombuffer(f.read(), np.uint8)
+    g["payload"] = np.concatenate([np.array(meta["mac_header"], np.uint8), g["payload_text"]])
+    return g
+
+
+def payload(nbytes: int, seed: int) -> np.ndarray:
+    return np.random.default_rng(seed).integers(0, 256, nbytes, dtype=np.uint8)
+
+
+def cfg(base: dict, **kw) -> dict:
+    d = dict(base)
+    d.update(kw)
+    return d
+
+
+# Configs used across tests (D default, G golden, B 2048/QPSK, C 4096/16-QAM)
+D = O.DEFAULT
+G = O.GOLDEN
+B = O.CONFIG_B
+CC = O.CONFIG_C
+EXTRA = {
+    "D_qam64": cfg(O.DEFAULT, mod_type=6),
+    "D_qam256": cfg(O.DEFAULT, mod_type=8),
+    "D_qpsk": cfg(O.DEFAULT, mod_type=2),
+    "N1024_k4": cfg(O.DEFAULT, fft_size=1024, num_data_subc=512, num_pilot_subc=16, cp_size=256),
+    "N256_k2": cfg(O.DEFAULT, fft_size=256, num_data_subc=128, num_pilot_subc=8, cp_size=64, mod_type=2),
+    "N128_k4_s3": cfg(O.DEFAULT, fft_size=128, num_data_subc=64, num_pilot_subc=4, cp_size=16, num_symb=3),
+    "N64_k1": cfg(O.DEFAULT, fft_size=64, num_data_subc=32, num_pilot_subc=4, cp_size=16, mod_type=1,
+                  num_symb=2),
+    "D_s12_staged": cfg(O.DEFAULT, num_symb=12),
+    "D_s1": cfg(O.DEFAULT, num_symb=1),
+    "D_p2": cfg(O.DEFAULT, num_pilot_subc=2),
+    "D_cp0": cfg(O.DEFAULT, cp_size=0),
+}
+ALL_CONFIGS = {"D": D, "G": G, "B": B, "C": CC, **EXTRA}
+
+
+def rel_err(a, b) -> float:
+    a = np.asarray(a)
+    b = np.asarray(b)
+    if a.size == 0:
+        return 0.0
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-300))

@@ -1,0 +1,92 @@
+"""C-ABI host-side checks (no GPU compute): the library loads, exports every
+entry point include/ofdm_mi355x.h declares, and its config parser behaves like
+the reference's parse_config (config/parser.cpp:4-33)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+import ofdm_mi355x as M
+import oracle as O
+
+
+def header_functions():
+    with open(M.HEADER) as f:
+        text = f.read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(ofdm_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = M.lib()
+    declared = header_functions()
+    assert len(declared) >= 20
+    missing = [n for n in declared if not hasattr(L, n)]
+    assert missing == []
+    assert set(declared) == set(M.SIGNATURES), "python binding out of sync with the header"
+    assert L.ofdm_abi_version() == 1
+
+
+def test_params_default_is_committed_config():
+    p = M.params_default()
+    assert p.as_dict() == O.DEFAULT
+
+
+CFG_TEXT = """# comment line
+fft_size        = 2048
+  num_data_subc = 1024
+num_pilot_subc=32
+cp_size = 5 12
+modType = 2
+not a key value line
+T2_sin_f1 = -17
+"""
+
+
+def _ref_lookup(path, key):
+    v = C.c_long()
+    rc = O.ref().ref_parse_config(path.encode(), key.encode(), C.byref(v))
+    return rc, v.value
+
+
+@pytest.mark.skipif(not O.ref_available(), reason="reference parser not built here")
+def test_config_parser_matches_reference(tmp_path):
+    path = str(tmp_path / "cfg.txt")
+    with open(path, "w") as f:
+        f.write(CFG_TEXT)
+    p = M.params_from_config(path)
+    for key, field in (("fft_size", "fft_size"), ("num_data_subc", "num_data_subc"),
+                       ("num_pilot_subc", "num_pilot_subc"), ("cp_size", "cp_size"),
+                       ("modType", "mod_type"), ("T2_sin_f1", "t2_sin_f1"), ("num_symb", "num_symb")):
+        rc, v = _ref_lookup(path, key)
+        assert rc == 0
+        assert getattr(p, field) == v, key
+        assert M.config_lookup(path, key) == v
+    # the reference's committed config/config.txt
+    ref_cfg = "/root/reference/config/config.txt"
+    if os.path.exists(ref_cfg):
+        assert M.params_from_config(ref_cfg).as_dict() == O.DEFAULT
+
+
+def test_config_errors(tmp_path):
+    with pytest.raises(M.OfdmError) as e:
+        M.params_from_config(str(tmp_path / "missing.txt"))
+    assert e.value.code == -4 and "Cannot open config file" in str(e.value)
+    bad = tmp_path / "bad.txt"
+    bad.write_text("fft_size = abc\n")
+    with pytest.raises(M.OfdmError) as e:
+        M.params_from_config(str(bad))
+    assert e.value.code == -6
+    if O.ref_available():
+        assert _ref_lookup(str(bad), "fft_size")[0] == -6
+        assert _ref_lookup(str(tmp_path / "missing.txt"), "x")[0] == -4
+
+
+def test_create_without_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(M.OfdmError) as e:
+        M.Modem(O.DEFAULT)
+    assert e.value.code in (-3,)

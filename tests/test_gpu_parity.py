@@ -1,0 +1,226 @@
+"""GPU parity: the HIP path (through the C-ABI) against the oracle on the same
+seeded inputs, against the reference's golden files, and — at BASELINE.json's
+full size — through size-independent properties (loopback round trip, BER).
+
+Tolerances (BASELINE.json north_star): demod decisions / bytes / int16 wire
+samples bit-exact; complex IQ and constellation within 1e-6 relative (we
+assert 1e-10: both sides are FP64 and differ only by FFT rounding order).
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from common import ALL_CONFIGS, B, CC, G, golden, payload, rel_err
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import ofdm_mi355x as M  # noqa: E402
+
+TOL = 1e-10
+_modems = {}
+
+
+def modem(name_or_cfg):
+    key = name_or_cfg if isinstance(name_or_cfg, str) else repr(sorted(name_or_cfg.items()))
+    if key not in _modems:
+        cfg = ALL_CONFIGS[name_or_cfg] if isinstance(name_or_cfg, str) else name_or_cfg
+        _modems[key] = M.Modem(cfg, 0)
+    return _modems[key]
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+NFR = {"B": 3, "C": 2}
+CFGS = sorted(ALL_CONFIGS)
+
+
+@pytest.mark.parametrize("name", CFGS)
+def test_tx_matches_oracle(name):
+    cfg = ALL_CONFIGS[name]
+    m = modem(name)
+    g = O.geometry(cfg)
+    nf = NFR.get(name, 4)
+    data = payload(nf * g["bytes_per_frame"], seed=hash(name) & 0xFFFF)
+    stride = g["message_len"] + 7  # non-contiguous frames
+    iq = torch.full((nf * stride,), complex(9.0, 9.0), dtype=torch.complex128, device="cuda")
+    iq16 = torch.zeros((nf * stride * 2,), dtype=torch.int16, device="cuda")
+    m.tx(dev(data), nf, iq, frame_stride=stride, iq16_out=iq16)
+    got = host(iq).reshape(nf, stride)
+    got16 = host(iq16).reshape(nf, stride * 2)
+    ref = O.tx_batch(cfg, data, nf, stride).copy()
+    ref = np.concatenate([ref, np.zeros(nf * stride - len(ref), np.complex128)]).reshape(nf, stride)
+    L = g["message_len"]
+    assert rel_err(got[:, :L], ref[:, :L]) < TOL
+    assert np.all(got[:, L:] == complex(9.0, 9.0)), "gap between frames must be untouched"
+    ref16 = np.stack([O.get_int16(ref[f, :L], cfg["mult"]) for f in range(nf)])
+    assert np.array_equal(got16[:, : 2 * L], ref16)
+
+
+def test_tx_frames_regenerate_source_bin():
+    gd = golden()
+    m = modem("G")
+    g = O.geometry(G)
+    fr = torch.zeros((g["frame_len"],), dtype=torch.complex128, device="cuda")
+    fr16 = torch.zeros((2 * g["frame_len"],), dtype=torch.int16, device="cuda")
+    m.tx_frames(dev(gd["payload"]), 1, fr, fr16)
+    assert np.array_equal(host(fr16), gd["source"])  # reference data/source.bin, bit-exact
+    assert rel_err(host(fr), O.frame_write(G, gd["payload"])) < TOL
+    # constants exposed for FRAME_FORM::preamble / t2sin
+    b, pre, modp, tpl = m.preamble()
+    assert list(b) == gd["preamble_bytes"]
+    opre, omodp, otpl = O.preamble_setup(G)
+    assert rel_err(pre, opre) < TOL and np.array_equal(modp, omodp) and rel_err(tpl, otpl) < TOL
+    assert rel_err(m.t2_symbol(), O.t2_symbol(G)) < TOL
+
+
+@pytest.mark.parametrize("name", CFGS)
+@pytest.mark.parametrize("snr_db", [None, 12.0])
+def test_rx_matches_oracle(name, snr_db):
+    cfg = ALL_CONFIGS[name]
+    m = modem(name)
+    g = O.geometry(cfg)
+    nf = NFR.get(name, 4)
+    data = payload(nf * g["bytes_per_frame"], seed=7 + len(name))
+    stride = g["message_len"] + 3
+    iq = O.tx_batch(cfg, data, nf, stride)
+    iq = np.concatenate([iq, np.zeros(nf * stride - len(iq), np.complex128)])
+    if snr_db is not None:
+        es = np.mean(np.abs(O.constellation(cfg["mod_type"])) ** 2)
+        iq = O.awgn(iq, np.sqrt(es / 10 ** (snr_db / 10)), seed=99)
+    cons = torch.zeros((nf * g["npts"],), dtype=torch.complex128, device="cuda")
+    out = torch.zeros((nf * g["bytes_per_frame"],), dtype=torch.uint8, device="cuda")
+    errs = torch.zeros((1,), dtype=torch.int64, device="cuda")
+    m.rx(dev(iq), nf, frame_stride=stride, constell_out=cons, bytes_out=out, ref=dev(data), bit_errors=errs)
+    ocons, obytes, oerrs = O.rx_batch(cfg, iq, nf, stride, ref=data)
+    assert rel_err(host(cons), ocons) < TOL
+    assert np.array_equal(host(out), obytes)
+    assert int(host(errs)[0]) == oerrs
+    if snr_db is None:
+        assert oerrs == 0 and np.array_equal(obytes, data)
+
+
+def test_rx_bytes_only_and_constell_only():
+    cfg = B
+    m = modem("B")
+    g = O.geometry(cfg)
+    nf = 5
+    data = payload(nf * g["bytes_per_frame"], seed=3)
+    iq = O.awgn(O.tx_batch(cfg, data, nf), 0.3, seed=5)
+    ocons, obytes, _ = O.rx_batch(cfg, iq, nf, g["message_len"])
+    out = torch.zeros((nf * g["bytes_per_frame"],), dtype=torch.uint8, device="cuda")
+    m.rx(dev(iq), nf, bytes_out=out)
+    assert np.array_equal(host(out), obytes)
+    cons = torch.zeros((nf * g["npts"],), dtype=torch.complex128, device="cuda")
+    m.rx(dev(iq), nf, constell_out=cons)
+    assert rel_err(host(cons), ocons) < TOL
+
+
+def test_rx_golden_capture_with_channel_estimate():
+    """data/constell.bin: the reference's equalised constellation of frame 1,
+    fed through the GPU rx with the golden chan_char_lq divisor (main.cpp:66-71)."""
+    gd = golden()
+    g = O.geometry(G)
+    x = gd["data"]
+    pr = gd["preamble_begin"][0]
+    mwp = x[pr: pr + g["preamble_len"] + g["message_len"]].copy()
+    pre, modp, _ = O.preamble_setup(G)
+    mwp = O.freq_shift(mwp, gd["cfo_frame1"])
+    mwp = O.cp_freq_sinh(G, mwp)
+    mwp = O.pr_phase_sinh(mwp, pre)
+    msg = np.ascontiguousarray(mwp[g["preamble_len"]:])
+    m = modem("G")
+    cons = torch.zeros((g["npts"],), dtype=torch.complex128, device="cuda")
+    out = torch.zeros((g["bytes_per_frame"],), dtype=torch.uint8, device="cuda")
+    m.rx(dev(msg), 1, chan=dev(gd["phases"]), constell_out=cons, bytes_out=out)
+    assert rel_err(host(cons), gd["constell"]) < 1e-6
+    assert np.abs(host(cons) - gd["constell"]).max() < 1e-12
+    assert np.array_equal(host(out), gd["payload"])
+
+
+@pytest.mark.parametrize("k", [1, 2, 4, 6, 8])
+def test_demap_and_map_match_oracle(k):
+    cfg = dict(ALL_CONFIGS["D"], mod_type=k)
+    m = modem(cfg)
+    rng = np.random.default_rng(k)
+    n = 1000 + k
+    pts = (rng.standard_normal(n) + 1j * rng.standard_normal(n)) * 0.8
+    pts[:3] = [0.0, 1.0 / 3.0 + 1j, -3.0 - 3j]
+    t = dev(pts)
+    nb = (n * k + 7) // 8
+    out = torch.zeros((nb,), dtype=torch.uint8, device="cuda")
+    m.demap(t, n, out)
+    ob, opts = O.demod(k, pts)
+    assert np.array_equal(host(out), ob)
+    assert np.array_equal(host(t), opts)  # clamped in place, like Modulation::demod
+    data = payload(333, seed=k)
+    npts = (333 * 8 + k - 1) // k
+    pts_out = torch.zeros((npts,), dtype=torch.complex128, device="cuda")
+    m.map(dev(data), 333, pts_out)
+    assert np.array_equal(host(pts_out), O.mod(k, data))
+
+
+def test_full_size_loopback_config_b():
+    """BASELINE config 2 at full size (65 536 symbols = 8 192 frames): tx then rx
+    on the GPU; clean channel decodes every byte, AWGN BER is in the expected band,
+    and a sample of frames equals the oracle on the same noisy samples."""
+    m = modem("B")
+    g = O.geometry(B)
+    nf = 8192
+    data = payload(nf * g["bytes_per_frame"], seed=2024)
+    d_data = dev(data)
+    iq = torch.empty((nf * g["message_len"],), dtype=torch.complex128, device="cuda")
+    out = torch.empty((nf * g["bytes_per_frame"],), dtype=torch.uint8, device="cuda")
+    errs = torch.zeros((1,), dtype=torch.int64, device="cuda")
+    m.tx(d_data, nf, iq)
+    m.rx(iq, nf, bytes_out=out, ref=d_data, bit_errors=errs)
+    assert int(host(errs)[0]) == 0
+    assert torch.equal(out, d_data)
+    # Es/N0 = 10 dB QPSK (constellation energy 2)
+    errs.zero_()
+    m.tx(d_data, nf, iq, noise_std=float(np.sqrt(2.0 / 10.0)), seed=11)
+    m.rx(iq, nf, bytes_out=out, ref=d_data, bit_errors=errs)
+    ber = int(host(errs)[0]) / (8.0 * len(data))
+    assert 3e-4 < ber < 5e-3, ber
+    idx = [0, 1, 4095, 8191]
+    h = host(iq).reshape(nf, g["message_len"])
+    hb = host(out).reshape(nf, -1)
+    for f in idx:
+        _, ob, _ = O.rx_batch(B, h[f], 1, g["message_len"])
+        assert np.array_equal(ob, hb[f])
+    # the GPU noise equals the oracle's counter-based noise
+    clean = O.tx_batch(B, data[: g["bytes_per_frame"]], 1)
+    noisy = O.awgn(clean, float(np.sqrt(2.0 / 10.0)), seed=11)
+    assert rel_err(h[0], noisy) < TOL
+
+
+def test_full_size_config_c_roundtrip():
+    m = modem("C")
+    g = O.geometry(CC)
+    nf = 2048
+    data = payload(nf * g["bytes_per_frame"], seed=77)
+    d = dev(data)
+    iq = torch.empty((nf * g["message_len"],), dtype=torch.complex128, device="cuda")
+    out = torch.empty_like(d)
+    m.tx(d, nf, iq)
+    m.rx(iq, nf, bytes_out=out)
+    assert torch.equal(out, d)
+
+
+def test_invalid_arguments_raise():
+    m = modem("D")
+    g = O.geometry(ALL_CONFIGS["D"])
+    iq = torch.zeros((g["message_len"],), dtype=torch.complex128, device="cuda")
+    with pytest.raises(M.OfdmError):
+        m.rx(iq, 1, frame_stride=g["message_len"] - 1)
+    with pytest.raises(M.OfdmError):
+        M.Modem(dict(ALL_CONFIGS["D"], fft_size=500))
+    with pytest.raises(M.OfdmError):
+        M.Modem(dict(ALL_CONFIGS["D"], mod_type=3))

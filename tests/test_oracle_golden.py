@@ -1,0 +1,77 @@
+"""Pin the oracle (oracle/ofdm_oracle.c) to the reference's golden files.
+
+Fixtures: tests/golden/ (made by tests/golden/make_golden.py from the
+reference's data/*.bin + data.txt: one BPSK main.cpp run, main.cpp:74-78,106-108).
+"""
+import numpy as np
+
+import oracle as O
+from common import G, golden, rel_err
+
+GD = golden()
+
+
+def test_preamble_bytes_match_reference_run():
+    # PREAMBLE_FORM ctor, Frame.cpp:269-272 (mt19937(42) + uniform_int_distribution<int>(0,255))
+    assert list(O.preamble_bytes(G)) == GD["preamble_bytes"]
+
+
+def test_tx_frame_regenerates_source_bin_bit_exact():
+    # FRAME_FORM::write + get_int16 (Frame.cpp:235-256) of the golden payload == data/source.bin
+    fr = O.frame_write(G, GD["payload"])
+    i16 = O.get_int16(fr, G["mult"])
+    assert np.array_equal(i16, GD["source"])
+
+
+def test_t2_corr_matches_reference():
+    corr = O.t2_corr(G, GD["data"])  # T2SIN_FORM::corr, Frame.hpp:96-147
+    assert corr.shape == GD["t2_corr"].shape
+    assert np.abs(corr - GD["t2_corr"]).max() < 1e-12
+    assert list(np.nonzero(corr)[0]) == GD["t2_blocks"]
+
+
+def _sync_chain(x, pos):
+    """main.cpp:51-71 replay: t2 find, preamble find(+1), copy, sync, equalise."""
+    t2 = O.find_t2sin(G, x, pos)
+    pre, modp, templ = O.preamble_setup(G)
+    pr = O.find_preamble(G, x, t2, templ) + 1
+    g = O.geometry(G)
+    frame = x[pr - G["t2sin_size"]: pr - G["t2sin_size"] + g["frame_len"]].copy()
+    mwp = frame[G["t2sin_size"]:]
+    cfo = O.pilot_freq_sinh(G, mwp[: g["preamble_len"]])
+    mwp = O.freq_shift(mwp, cfo)
+    mwp = O.cp_freq_sinh(G, mwp)
+    mwp = O.pr_phase_sinh(mwp, pre)
+    chan = O.chan_char_lq(G, mwp[: g["preamble_len"]], modp)
+    cons = O.ofdm_fft(G, mwp[g["preamble_len"]:]) / np.tile(chan, G["num_symb"])
+    return t2, pr, cfo, chan, cons
+
+
+def test_rx_chain_frame1_matches_goldens():
+    t2, pr, cfo, chan, cons = _sync_chain(GD["data"], 0)
+    assert t2 == GD["t2_first_block_start"]
+    assert pr == GD["preamble_begin"][0]
+    assert cfo == GD["cfo_frame1"]
+    assert np.abs(chan - GD["phases"]).max() < 1e-12                  # data/phases.bin
+    assert rel_err(cons, GD["constell"]) < 1e-12                       # data/constell.bin
+    assert np.abs(cons - GD["constell"]).max() / np.abs(GD["constell"]).min() < 1e-12
+    b, _ = O.demod(1, cons)
+    assert np.array_equal(b, GD["payload"])                             # data.txt + MAC header
+
+
+def test_rx_chain_frame2_decodes():
+    # second frame of the capture (rx.cpp streaming continues after the first)
+    _, pr1, *_ = _sync_chain(GD["data"], 0)
+    g = O.geometry(G)
+    t2, pr, cfo, chan, cons = _sync_chain(GD["data"], pr1 + g["message_len"])
+    assert pr == GD["preamble_begin"][1]
+    b, _ = O.demod(1, cons)
+    assert np.array_equal(b, GD["payload"])
+
+
+def test_fft_is_the_dft_definition():
+    rng = np.random.default_rng(1)
+    for n in (8, 64, 256, 512, 640, 2048, 2560, 12, 17):
+        x = rng.standard_normal(n) + 1j * rng.standard_normal(n)
+        assert rel_err(O.fft(x, -1), np.fft.fft(x)) < 1e-13
+        assert rel_err(O.fft(x, +1), np.fft.ifft(x) * n) < 1e-13
