@@ -9,10 +9,16 @@
 // Shape: one workgroup of T = N/8 threads per transform. Every pass is a
 // Stockham auto-sort radix-8 pass (last pass radix 2 or 4 when LOGN%3 != 0).
 // Thread t always holds in[t + T*i], i = 0..7, so the first pass reads
-// straight from HBM with 16-B coalesced loads; intermediate passes exchange
-// through LDS (16-B ds_read/ds_write_b128), padded by one 16-B slot every 8
-// elements so the stride-8 writes of the first pass are bank-conflict free.
-// Twiddles come from a per-context table W_N^j (global, L1/L2 resident).
+// straight from HBM (or an LDS-DMA stage) with 16-B coalesced accesses;
+// intermediate passes exchange through LDS (ds_read/ds_write_b128), padded
+// by one 16-B slot every 8 elements so the stride-8 writes of the first pass
+// are bank-conflict free.
+//
+// Twiddles live in LDS as a two-level table W_N^j = HI[j>>6] * LO[j&63]
+// (N/64 + 64 entries, ~1.5 KiB at N=2048): the FFT issues no global loads,
+// so an LDS-DMA prefetch of the next symbol stays in flight across it, and the
+// workgroup barriers are raw s_barrier + lgkmcnt(0) (a __syncthreads()
+// would add vmcnt(0) and drain that prefetch).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -65,6 +71,42 @@ __device__ __forceinline__ double2 mul_j(double2 a)
 
 __device__ __forceinline__ int lds_pad(int e) { return e + (e >> 3); }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS
+// operations, not for its vector-memory queue (so stores and LDS-DMA issued
+// earlier stay in flight).
+__device__ __forceinline__ void lds_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// ---------------------------------------------------------------- twiddles
+template <int LOGN>
+struct TwLds {
+    static constexpr int N = 1 << LOGN;
+    static constexpr int NHI = N / 64;          // >= 1 for N >= 64
+    static constexpr int SIZE = NHI + 64;       // double2 entries in LDS
+};
+
+// Fill the two-level table from the context's global W_N^j table.
+template <int LOGN>
+__device__ __forceinline__ void load_twiddles(const double2* __restrict__ tw, double2* __restrict__ lds_tw, int t,
+                                              int nthreads)
+{
+    constexpr int NHI = TwLds<LOGN>::NHI;
+    for (int i = t; i < NHI + 64; i += nthreads) lds_tw[i] = i < NHI ? tw[i * 64] : tw[i - NHI];
+}
+
+// W_N^j (forward sign) from the LDS table.
+template <int LOGN>
+__device__ __forceinline__ double2 tw_get(const double2* __restrict__ lds_tw, int j)
+{
+    constexpr int NHI = TwLds<LOGN>::NHI;
+    if constexpr (NHI == 1) return lds_tw[1 + j];
+    return cmul(lds_tw[j >> 6], lds_tw[NHI + (j & 63)]);
+}
+
 // ---------------------------------------------------------------- DFTs
 template <int SIGN>
 __device__ __forceinline__ void dft2(double2& a, double2& b)
@@ -114,14 +156,13 @@ struct FftShape {
     static constexpr int T = N / 8;            // threads per transform
     static constexpr int NPASS8 = LOGN / 3;    // radix-8 passes
     static constexpr int REM = LOGN % 3;       // trailing radix-2/4 pass
-    static constexpr int LAST_NS = 1 << (3 * NPASS8);
     static constexpr int PADN = N + N / 8;     // padded LDS elements
 };
 
-// One Stockham pass, radix R, input span Ns. v[i] holds in[t + T*i].
-// Twiddle table tw[j] = exp(-2*pi*i*j/N) (forward); conjugated for SIGN>0.
+// One Stockham pass, radix R, input span NS. v[i] holds in[t + T*i].
+// Twiddle powers w^r, r < R, of w = W_N^(k*N/(NS*R)) from the LDS table.
 template <int LOGN, int R, int NS, int SIGN>
-__device__ __forceinline__ void stockham_pass(double2 (&v)[8], int t, const double2* __restrict__ tw,
+__device__ __forceinline__ void stockham_pass(double2 (&v)[8], int t, const double2* __restrict__ lds_tw,
                                               double2* __restrict__ lds)
 {
     constexpr int N = 1 << LOGN, T = N / 8, B = 8 / R;
@@ -130,12 +171,22 @@ __device__ __forceinline__ void stockham_pass(double2 (&v)[8], int t, const doub
         const int b = t + T * u;
         const int k = b & (NS - 1);
         if constexpr (NS > 1) {
-#pragma unroll
-            for (int r = 1; r < R; ++r) {
-                double2 w = tw[k * r * (N / (NS * R))];
-                if (SIGN > 0) w.y = -w.y;
-                v[u + r * B] = cmul(v[u + r * B], w);
+            double2 w1 = tw_get<LOGN>(lds_tw, k * (N / (NS * R)));
+            if (SIGN > 0) w1.y = -w1.y;
+            double2 w[8];
+            w[1] = w1;
+            if constexpr (R >= 4) {
+                w[2] = cmul(w1, w1);
+                w[3] = cmul(w[2], w1);
             }
+            if constexpr (R == 8) {
+                w[4] = cmul(w[2], w[2]);
+                w[5] = cmul(w[4], w1);
+                w[6] = cmul(w[3], w[3]);
+                w[7] = cmul(w[4], w[3]);
+            }
+#pragma unroll
+            for (int r = 1; r < R; ++r) v[u + r * B] = cmul(v[u + r * B], w[r]);
         }
         if constexpr (R == 8)
             dft8<SIGN>(v[u], v[u + B], v[u + 2 * B], v[u + 3 * B], v[u + 4 * B], v[u + 5 * B],
@@ -160,7 +211,7 @@ __device__ __forceinline__ void lds_load8(double2 (&v)[8], int t, const double2*
 
 // Remaining passes after the first one has been written to `lds`.
 template <int LOGN, int PASS, int SIGN>
-__device__ __forceinline__ void fft_tail(double2 (&v)[8], int t, const double2* __restrict__ tw,
+__device__ __forceinline__ void fft_tail(double2 (&v)[8], int t, const double2* __restrict__ lds_tw,
                                          double2* __restrict__ lds)
 {
     using S = FftShape<LOGN>;
@@ -169,25 +220,24 @@ __device__ __forceinline__ void fft_tail(double2 (&v)[8], int t, const double2* 
         constexpr bool is8 = PASS < S::NPASS8;
         constexpr int R = is8 ? 8 : (1 << S::REM);
         constexpr int NS = 1 << (3 * PASS);
-        __syncthreads();  // previous pass fully written
+        lds_barrier();  // previous pass fully written
         lds_load8<LOGN>(v, t, lds);
-        __syncthreads();  // everyone has read before the buffer is overwritten
-        stockham_pass<LOGN, R, NS, SIGN>(v, t, tw, lds);
-        fft_tail<LOGN, PASS + 1, SIGN>(v, t, tw, lds);
+        lds_barrier();  // everyone has read before the buffer is overwritten
+        stockham_pass<LOGN, R, NS, SIGN>(v, t, lds_tw, lds);
+        fft_tail<LOGN, PASS + 1, SIGN>(v, t, lds_tw, lds);
     }
 }
 
 // Full transform. On entry v[i] = x[t + T*i]; on exit the natural-order
 // result X[0..N) is in lds (padded indexing) and the workgroup is synced.
 template <int LOGN, int SIGN>
-__device__ __forceinline__ void fft_block(double2 (&v)[8], int t, const double2* __restrict__ tw,
+__device__ __forceinline__ void fft_block(double2 (&v)[8], int t, const double2* __restrict__ lds_tw,
                                           double2* __restrict__ lds)
 {
-    using S = FftShape<LOGN>;
     static_assert(LOGN >= 6 && LOGN <= 12, "N must be 64..4096");
-    stockham_pass<LOGN, 8, 1, SIGN>(v, t, tw, lds);
-    fft_tail<LOGN, 1, SIGN>(v, t, tw, lds);
-    __syncthreads();
+    stockham_pass<LOGN, 8, 1, SIGN>(v, t, lds_tw, lds);
+    fft_tail<LOGN, 1, SIGN>(v, t, lds_tw, lds);
+    lds_barrier();
 }
 
 }  // namespace ofdm

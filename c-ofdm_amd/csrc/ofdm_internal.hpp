@@ -64,5 +64,7 @@ hipError_t launch_map(const uint8_t* bytes, long nbytes, int k, const double2* t
 // Register-resident rx limits: S*ceil(D/T) <= RX_REG_SLOTS.
 constexpr int RX_SMAX = 8;
 constexpr int RX_DPT = 4;
+// tx: persistent grid-stride launch size (symbols per workgroup = nsym / grid)
+constexpr long TX_MAX_GRID = 4096;
 
 }  // namespace ofdm

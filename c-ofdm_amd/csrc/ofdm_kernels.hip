@@ -63,17 +63,19 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z)
     return z ^ (z >> 31);
 }
 
-// Counter-based Box-Muller AWGN (same definition as oracle orc_awgn).
+// Counter-based Box-Muller AWGN (same definition as oracle orc_awgn). A
+// channel model, not modem arithmetic: 24-bit uniforms and the gfx950 FP32
+// transcendental units (v_log_f32 = log2, v_sin/cos_f32 take revolutions),
+// ~10 VALU ops per sample instead of an FP64 log/sqrt/sincos (~200).
 __device__ __forceinline__ double2 awgn_sample(unsigned long long seed, unsigned long long g, double sc)
 {
     const uint64_t h1 = mix64(seed + 0x9E3779B97F4A7C15ull * (2 * g + 1));
     const uint64_t h2 = mix64(seed + 0x9E3779B97F4A7C15ull * (2 * g + 2));
-    const double u1 = (double)((h1 >> 11) + 1) * 0x1.0p-53;
-    const double u2 = (double)(h2 >> 11) * 0x1.0p-53;
-    const double r = sqrt(-2.0 * log(u1)) * sc;
-    double sn, cs;
-    sincos(2.0 * M_PI * u2, &sn, &cs);
-    return make_double2(r * cs, r * sn);
+    const float u1 = (float)((h1 >> 40) + 1) * 0x1.0p-24f;  // (0, 1]
+    const float u2 = (float)(h2 >> 40) * 0x1.0p-24f;        // [0, 1)
+    const float r = __builtin_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));  // sqrt(-2 ln u1)
+    const float c = __builtin_amdgcn_cosf(u2), s = __builtin_amdgcn_sinf(u2);           // of 2*pi*u2
+    return make_double2((double)(r * c) * sc, (double)(r * s) * sc);
 }
 
 __device__ __forceinline__ int16_t to_int16(double v) { return (int16_t)(int)v; }
@@ -118,74 +120,154 @@ __device__ __forceinline__ unsigned long long block_sum_u64(unsigned long long v
 }
 
 // ------------------------------------------------------------------ tx
+// Persistent over symbols: grid-stride loop, so the twiddle table and each
+// thread's bin classification are loaded once per workgroup, and the next
+// symbol's payload bytes are fetched into registers while this one is
+// transformed and written.
 template <int LOGN>
 __global__ void __launch_bounds__((1 << LOGN) / 8) tx_kernel(TxArgs a)
 {
     using FS = FftShape<LOGN>;
     constexpr int N = FS::N, T = FS::T;
     extern __shared__ double2 smem[];
+    double2* fft = smem;
+    double2* lds_tw = smem + FS::PADN;
+    double2* lds_const = lds_tw + TwLds<LOGN>::SIZE;                            // 2^k points
+    uint8_t* sbytes = reinterpret_cast<uint8_t*>(lds_const + 256);              // one symbol's payload
     const int t = threadIdx.x;
-    const long sym = blockIdx.x;
-    const long f = sym / a.S;
-    const int s = (int)(sym - f * a.S);
-    const uint8_t* fb = a.bytes + f * a.bytes_per_frame;
+    load_twiddles<LOGN>(a.tab.tw, lds_tw, t, T);
+    for (int i = t; i < (1 << a.k); i += T) lds_const[i] = a.tab.constell[i];
 
-    // FFT_FORM::write: zero, pilots = pilot_ampl, segments <- mapped points.
-    double2 v[8];
+    // FFT_FORM::write layout: bin -> data index / pilot / unused (Frame.cpp:31-44,54-62)
+    int kind[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int m = a.tab.bin_map[t + T * i];
-        if (m >= 0) {
-            const int val = symbol_bits(fb, a.bytes_per_frame, (long)s * a.D + m, a.k);
-            v[i] = a.tab.constell[val];
-        } else {
-            v[i] = make_double2(m == -2 ? a.pilot_ampl : 0.0, 0.0);
-        }
-    }
-    fft_block<LOGN, +1>(v, t, a.tab.tw, smem);
+    for (int i = 0; i < 8; ++i) kind[i] = a.tab.bin_map[t + T * i];
 
-    // body / sqrt(N) after a CP copy of its last cp samples (Frame.cpp:66-68,191-197)
+    const long nsym = a.nframes * a.S;
+    const int k = a.k;
+    const int bps = a.D * k / 8;  // payload bytes per symbol (host checks D*k % 8 == 0)
+    const double2 pil = make_double2(a.pilot_ampl, 0.0);
     const int L = N + a.cp;
-    const long base = f * a.frame_stride + a.msg_offset + (long)s * L;
-    double2* out = a.iq + base;
-    int16_t* out16 = a.iq16 ? a.iq16 + 2 * base : nullptr;
-    const unsigned long long g0 = a.sample_offset + (unsigned long long)(f * (long)a.S + s) * L;
-    for (int j = t; j < L; j += T) {
-        const int n = j < a.cp ? N - a.cp + j : j - a.cp;
-        double2 z = smem[lds_pad(n)];
-        z.x *= a.inv_sqrt_n;
-        z.y *= a.inv_sqrt_n;
-        if (out16) {
-            out16[2 * j] = to_int16(z.x * a.mult);
-            out16[2 * j + 1] = to_int16(z.y * a.mult);
-        }
-        if (a.noise_scale > 0.0) {
-            const double2 w = awgn_sample(a.seed, g0 + j, a.noise_scale);
-            z.x += w.x;
-            z.y += w.y;
-        }
-        out[j] = z;
+    auto sym_bytes = [&](long sym) {
+        const long f = sym / a.S;
+        return a.bytes + f * a.bytes_per_frame + (sym - f * a.S) * bps;
+    };
+
+    // Coalesced payload prefetch: thread t holds bytes t + T*r of the next
+    // symbol (bps <= N = 8T); they are written to LDS only at the end of the
+    // iteration, so the loads' latency hides behind the FFT.
+    uint8_t nb[8];
+    long sym = blockIdx.x;
+    if (sym < nsym) {
+        const uint8_t* src = sym_bytes(sym);
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+            if (t + T * r < bps) sbytes[t + T * r] = src[t + T * r];
     }
-    // [T2 | preamble] header of full FRAME_FORM buffers (Frame.cpp:219,228-229)
-    if (a.header && s == 0) {
-        double2* fr = a.iq + f * a.frame_stride;
-        int16_t* fr16 = a.iq16 ? a.iq16 + 2 * f * a.frame_stride : nullptr;
-        for (int j = t; j < a.header_len; j += T) {
-            const double2 z = a.header[j];
-            fr[j] = z;
-            if (fr16) {
-                fr16[2 * j] = to_int16(z.x * a.mult);
-                fr16[2 * j + 1] = to_int16(z.y * a.mult);
+    lds_barrier();  // twiddle table + first payload visible
+
+    for (; sym < nsym; sym += gridDim.x) {
+        const long f = sym / a.S;
+        const int s = (int)(sym - f * a.S);
+        // Modulation::mod: k-bit symbol -> constellation point (modulation.cpp:39-50)
+        double2 v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            if (kind[i] >= 0) {
+                const int bit = kind[i] * k;
+                const int byte = bit >> 3, off = bit & 7;
+                const int w = ((int)sbytes[byte] << 8) | (off + k > 8 ? (int)sbytes[byte + 1] : 0);
+                v[i] = lds_const[(w >> (16 - off - k)) & ((1 << k) - 1)];
+            } else {
+                v[i] = kind[i] == -2 ? pil : make_double2(0.0, 0.0);
             }
         }
+        const long nxt = sym + gridDim.x;
+        const uint8_t* nsrc = sym_bytes(nxt < nsym ? nxt : sym);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) nb[r] = nsrc[t + T * r < bps ? t + T * r : 0];
+
+        fft_block<LOGN, +1>(v, t, lds_tw, fft);
+
+        // body / sqrt(N) after a CP copy of its last cp samples (Frame.cpp:66-68,191-197)
+        const long base = f * a.frame_stride + a.msg_offset + (long)s * L;
+        double2* out = a.iq + base;
+        int16_t* out16 = a.iq16 ? a.iq16 + 2 * base : nullptr;
+        const unsigned long long g0 = a.sample_offset + (unsigned long long)sym * L;
+        for (int j = t; j < L; j += T) {
+            const int n = j < a.cp ? N - a.cp + j : j - a.cp;
+            double2 z = fft[lds_pad(n)];
+            z.x *= a.inv_sqrt_n;
+            z.y *= a.inv_sqrt_n;
+            if (out16) {
+                out16[2 * j] = to_int16(z.x * a.mult);
+                out16[2 * j + 1] = to_int16(z.y * a.mult);
+            }
+            if (a.noise_scale > 0.0) {
+                const double2 w = awgn_sample(a.seed, g0 + j, a.noise_scale);
+                z.x += w.x;
+                z.y += w.y;
+            }
+            out[j] = z;
+        }
+        // [T2 | preamble] header of full FRAME_FORM buffers (Frame.cpp:219,228-229)
+        if (a.header && s == 0) {
+            double2* fr = a.iq + f * a.frame_stride;
+            int16_t* fr16 = a.iq16 ? a.iq16 + 2 * f * a.frame_stride : nullptr;
+            for (int j = t; j < a.header_len; j += T) {
+                const double2 z = a.header[j];
+                fr[j] = z;
+                if (fr16) {
+                    fr16[2 * j] = to_int16(z.x * a.mult);
+                    fr16[2 * j + 1] = to_int16(z.y * a.mult);
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+            if (t + T * r < bps) sbytes[t + T * r] = nb[r];
+        lds_barrier();  // next payload visible; fft[] output reads precede the next pass 0
     }
 }
 
 // ------------------------------------------------------------------ rx
+// One workgroup per frame. Symbol s+1 streams HBM -> LDS stage by LDS-DMA
+// (global_load_lds_dwordx4) while symbol s is transformed, so the load of the
+// next symbol overlaps the FFT with no extra VGPRs.
 // STAGED=false: the frame's S*D equalisation inputs live in VGPRs
-//   (S <= RX_SMAX, D <= RX_DPT*T). A rolled symbol loop shifts them through a
+//   (S <= RX_SMAX, D <= RX_DPT*T); a rolled symbol loop shifts them through a
 //   fixed register window so every register index stays compile-time.
-// STAGED=true: any S; inputs parked in a_.ystage (same-thread re-read).
+// STAGED=true: any S; inputs parked in a.ystage (same-thread re-read).
+// The DMA is issued through inline asm (MI355X guide §5.7 LDS-DMA recipe:
+// save M0, M0 = wave-uniform LDS byte address, global_load_lds_dwordx4,
+// restore M0). hipcc cannot prove the stage and the FFT buffer disjoint and
+// would otherwise wait vmcnt(0) before the first FFT ds_write, draining the
+// prefetch; the kernel's own `s_waitcnt vmcnt(0)` before reading the stage is
+// the only wait the DMA needs (no other vector-memory ops are in flight then).
+template <int LOGN>
+__device__ __forceinline__ void dma_symbol(const double2* __restrict__ src, double2* stage, int t)
+{
+    constexpr int T = (1 << LOGN) / 8;
+    const int w0 = t & ~63;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int e0 = w0 + T * i;  // wave-uniform: the wave's 64 lanes land contiguously
+        const double2* g = src + e0 + (t & 63);
+        const unsigned lds = __builtin_amdgcn_readfirstlane(
+            (unsigned)(uintptr_t)(__attribute__((address_space(3))) double2*)(stage + e0));
+        unsigned keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %2\n\t"
+            "s_nop 0\n\t"
+            "global_load_lds_dwordx4 %1, off\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(g), "s"(lds)
+            : "memory");
+    }
+}
+
 template <int LOGN, bool STAGED>
 __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
 {
@@ -194,17 +276,21 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
     constexpr int SW = STAGED ? 1 : RX_SMAX;  // register window (symbols)
     extern __shared__ double2 smem[];
     const int S = a.S, D = a.D, P = a.P;
-    double2* lds = smem;
-    double2* pil = smem + FS::PADN;       // S*P raw pilots
-    double2* gain = pil + S * P;          // S*P equaliser gains
+    double2* stage = smem;                  // N raw samples (DMA target)
+    double2* fft = stage + N;               // PADN
+    double2* lds_tw = fft + FS::PADN;       // TwLds::SIZE
+    double2* pil = lds_tw + TwLds<LOGN>::SIZE;  // S*P raw pilots
+    double2* gain = pil + S * P;            // S*P equaliser gains
     double* red = reinterpret_cast<double*>(gain + S * P);
-    uint8_t* dec = reinterpret_cast<uint8_t*>(smem);  // aliases lds after the FFTs
+    uint8_t* dec = reinterpret_cast<uint8_t*>(fft);  // aliases fft after the transforms
 
     const int t = threadIdx.x;
     const long f = blockIdx.x;
     const int L = N + a.cp;
-    const double2* x = a.iq + f * a.frame_stride;
+    const double2* x = a.iq + f * a.frame_stride + a.cp;  // CP strip (Frame.hpp:278-279)
 
+    dma_symbol<LOGN>(x, stage, t);
+    load_twiddles<LOGN>(a.tab.tw, lds_tw, t, T);
     int bins[RX_DPT], slot[RX_DPT];
 #pragma unroll
     for (int i = 0; i < RX_DPT; ++i) {
@@ -212,21 +298,25 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
         bins[i] = d < D ? a.tab.data_bin[d] : 0;
         slot[i] = d < D ? a.tab.data_slot[d] : 0;
     }
+    const int pbin = t < P ? a.tab.pilot_bin[t] : 0;
 
     double2 y[SW][RX_DPT];
 #pragma unroll 1
     for (int s = 0; s < S; ++s) {
-        const double2* sym = x + (long)s * L + a.cp;  // CP strip
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of symbol s landed
+        lds_barrier();                                     // ... and every other wave's
         double2 v[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = sym[t + T * i];
-        fft_block<LOGN, -1>(v, t, a.tab.tw, lds);
-        for (int j = t; j < P; j += T) pil[s * P + j] = lds[lds_pad(a.tab.pilot_bin[j])];
+        for (int i = 0; i < 8; ++i) v[i] = stage[t + T * i];
+        lds_barrier();  // stage fully read: refill it with symbol s+1
+        if (s + 1 < S) dma_symbol<LOGN>(x + (long)(s + 1) * L, stage, t);
+        fft_block<LOGN, -1>(v, t, lds_tw, fft);
+        if (t < P) pil[s * P + t] = fft[lds_pad(pbin)];
         if constexpr (STAGED) {
 #pragma unroll
             for (int i = 0; i < RX_DPT; ++i) {
                 const int d = t + T * i;
-                if (d < D) a.ystage[(f * S + s) * D + d] = lds[lds_pad(bins[i])];
+                if (d < D) a.ystage[(f * S + s) * D + d] = fft[lds_pad(bins[i])];
             }
         } else {
 #pragma unroll
@@ -234,10 +324,11 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
 #pragma unroll
                 for (int i = 0; i < RX_DPT; ++i) y[w][i] = y[w + 1][i];
 #pragma unroll
-            for (int i = 0; i < RX_DPT; ++i) y[SW - 1][i] = lds[lds_pad(bins[i])];
+            for (int i = 0; i < RX_DPT; ++i) y[SW - 1][i] = fft[lds_pad(bins[i])];
         }
-        __syncthreads();  // lds reused by the next symbol
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
 
     // phys_pilot_ampl = sum |pilot| / (P*S*pilot_ampl)   (Frame.cpp:76-80)
     double acc = 0.0;
@@ -310,17 +401,12 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
             for (int i = 0; i < RX_DPT; ++i)
                 if (t + T * i < D) emit(s, i, a.ystage[(f * S + s) * D + t + T * i]);
             __syncthreads();
-            if (whole_frame_dec)
-                ;  // packed once below
-            else {
+            if (!whole_frame_dec) {
                 pack(s * bps, (s + 1) * bps, 0);
                 __syncthreads();
             }
         }
-        if (whole_frame_dec) {
-            __syncthreads();
-            pack(0, bpf, 0);
-        }
+        if (whole_frame_dec) pack(0, bpf, 0);
     }
     if (a.bit_errors) {
         errs = block_sum_u64<T>(errs, red);
@@ -371,14 +457,16 @@ template <int LOGN>
 static hipError_t tx_launch_n(const TxArgs& a, hipStream_t st)
 {
     using FS = FftShape<LOGN>;
-    const size_t shm = sizeof(double2) * FS::PADN;
+    const size_t shm = sizeof(double2) * (FS::PADN + TwLds<LOGN>::SIZE + 256) + FS::N;  // + table + payload
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)tx_kernel<LOGN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
         attr = true;
     }
-    const long grid = a.nframes * a.S;
-    if (grid <= 0) return hipSuccess;
+    const long nsym = a.nframes * a.S;
+    if (nsym <= 0) return hipSuccess;
+    // persistent grid: enough workgroups to fill every CU several times over
+    const long grid = nsym < TX_MAX_GRID ? nsym : TX_MAX_GRID;
     hipLaunchKernelGGL(tx_kernel<LOGN>, dim3((unsigned)grid), dim3(FS::T), shm, st, a);
     return hipGetLastError();
 }
@@ -401,7 +489,7 @@ template <int LOGN>
 static size_t rx_shm(const RxArgs& a)
 {
     using FS = FftShape<LOGN>;
-    return sizeof(double2) * (FS::PADN + 2 * (size_t)a.S * a.P) + 32 * sizeof(double);
+    return sizeof(double2) * (FS::N + FS::PADN + TwLds<LOGN>::SIZE + 2 * (size_t)a.S * a.P) + 32 * sizeof(double);
 }
 
 template <int LOGN, bool STAGED>
@@ -427,6 +515,7 @@ static hipError_t rx_dispatch(const RxArgs& a, hipStream_t st, bool* staged)
     using FS = FftShape<LOGN>;
     const bool fits = a.S <= RX_SMAX && a.D <= RX_DPT * FS::T;
     if (staged) *staged = !fits;
+    if (a.P > FS::T) return hipErrorInvalidValue;
     if (!fits && a.ystage == nullptr) return hipErrorInvalidValue;
     return fits ? rx_launch_n<LOGN, false>(a, st) : rx_launch_n<LOGN, true>(a, st);
 }

@@ -727,7 +727,9 @@ static inline uint64_t mix64(uint64_t z)
     return z ^ (z >> 31);
 }
 
-/* Counter-based Box-Muller AWGN; same definition as the HIP tx kernel. */
+/* Counter-based Box-Muller AWGN; same definition as the HIP tx kernel (24-bit
+ * uniforms from splitmix64 of the sample counter). The GPU evaluates log/sin/
+ * cos on its FP32 units, so the two agree to ~1e-6 of noise_std, not bitwise. */
 void orc_awgn(double* xd, long n, double noise_std, unsigned long long seed,
               unsigned long long off)
 {
@@ -737,8 +739,8 @@ void orc_awgn(double* xd, long n, double noise_std, unsigned long long seed,
         uint64_t g = off + (uint64_t)i;
         uint64_t h1 = mix64(seed + 0x9E3779B97F4A7C15ull * (2 * g + 1));
         uint64_t h2 = mix64(seed + 0x9E3779B97F4A7C15ull * (2 * g + 2));
-        double u1 = (double)((h1 >> 11) + 1) * 0x1.0p-53;
-        double u2 = (double)(h2 >> 11) * 0x1.0p-53;
+        double u1 = (double)(float)((float)((h1 >> 40) + 1) * 0x1.0p-24f);
+        double u2 = (double)(float)((float)(h2 >> 40) * 0x1.0p-24f);
         double r = sqrt(-2.0 * log(u1)) * sc;
         double th = 2.0 * M_PI * u2;
         x[i] += CMPLX(r * cos(th), r * sin(th));

@@ -48,7 +48,7 @@ EXTRA = {
     "N256_k2": cfg(O.DEFAULT, fft_size=256, num_data_subc=128, num_pilot_subc=8, cp_size=64, mod_type=2),
     "N128_k4_s3": cfg(O.DEFAULT, fft_size=128, num_data_subc=64, num_pilot_subc=4, cp_size=16, num_symb=3),
     "N64_k1": cfg(O.DEFAULT, fft_size=64, num_data_subc=32, num_pilot_subc=4, cp_size=16, mod_type=1,
-                  num_symb=2),
+                  num_symb=2, pr_sin_len=64, t2sin_size=64, t2_sin_f1=5, t2_sin_f2=20, smooth=2),
     "D_s12_staged": cfg(O.DEFAULT, num_symb=12),
     "D_s1": cfg(O.DEFAULT, num_symb=1),
     "D_p2": cfg(O.DEFAULT, num_pilot_subc=2),

@@ -33,6 +33,23 @@ def dev(a):
     return torch.from_numpy(np.ascontiguousarray(a)).cuda()
 
 
+def assert_int16_match(got16, ref_iq, mult):
+    """int16 wire samples (FRAME_FORM::get_int16 = trunc(x*mult)) must be
+    identical, except where x*mult lies within 1e-9 of an integer: there the
+    truncation is decided by FFT rounding order (FFTW, oracle and GPU all
+    differ in the last ulp) and a 1-LSB difference is allowed."""
+    v = np.empty(2 * ref_iq.size)
+    v[0::2] = ref_iq.real.ravel() * mult
+    v[1::2] = ref_iq.imag.ravel() * mult
+    got = got16.ravel().astype(np.int64)
+    want = np.trunc(v).astype(np.int64)
+    diff = got != want
+    ambiguous = np.abs(v - np.round(v)) < 1e-9 * np.maximum(1.0, np.abs(v))
+    assert np.all(ambiguous[diff]), f"{int((diff & ~ambiguous).sum())} non-ambiguous int16 mismatches"
+    assert np.all(np.abs(got - want)[diff] <= 1)
+    return int(diff.sum())
+
+
 def host(t):
     torch.cuda.synchronize()
     return t.cpu().numpy()
@@ -60,8 +77,7 @@ def test_tx_matches_oracle(name):
     L = g["message_len"]
     assert rel_err(got[:, :L], ref[:, :L]) < TOL
     assert np.all(got[:, L:] == complex(9.0, 9.0)), "gap between frames must be untouched"
-    ref16 = np.stack([O.get_int16(ref[f, :L], cfg["mult"]) for f in range(nf)])
-    assert np.array_equal(got16[:, : 2 * L], ref16)
+    assert_int16_match(got16[:, : 2 * L], ref[:, :L], cfg["mult"])
 
 
 def test_tx_frames_regenerate_source_bin():
@@ -198,7 +214,7 @@ def test_full_size_loopback_config_b():
     # the GPU noise equals the oracle's counter-based noise
     clean = O.tx_batch(B, data[: g["bytes_per_frame"]], 1)
     noisy = O.awgn(clean, float(np.sqrt(2.0 / 10.0)), seed=11)
-    assert rel_err(h[0], noisy) < TOL
+    assert rel_err(h[0], noisy) < 1e-5  # FP32 transcendental noise (channel model) vs FP64 oracle
 
 
 def test_full_size_config_c_roundtrip():
