@@ -10,12 +10,15 @@
 // Stockham auto-sort radix-8 pass (last pass radix 2 or 4 when LOGN%3 != 0).
 // Thread t always holds in[t + T*i], i = 0..7, so the first pass reads
 // straight from HBM (or an LDS-DMA stage) with 16-B coalesced accesses;
-// intermediate passes exchange through LDS (ds_read/ds_write_b128), padded
-// by one 16-B slot every 8 elements so the stride-8 writes of the first pass
-// are bank-conflict free.
+// intermediate passes exchange through LDS (ds_read/ds_write_b128). The LDS
+// image is XOR-swizzled, slot(e) = e ^ ((e >> 3) & 7): the stride-8 writes of
+// the first pass and the unit-stride reads of every pass are both
+// bank-conflict free under gfx950's ds_write_b128 (8-lane) and ds_read_b128
+// (16-lane) groups, with no padding (N x 16 B per transform).
 //
 // Twiddles live in LDS as a two-level table W_N^j = HI[j>>6] * LO[j&63]
-// (N/64 + 64 entries, ~1.5 KiB at N=2048): the FFT issues no global loads,
+// (N/64 + 64 entries, ~1.5 KiB at N=2048; LO stored at (j ^ ((j>>4)&3)),
+// which makes the strided LO reads of every pass conflict-free for N=64..4096): the FFT issues no global loads,
 // so an LDS-DMA prefetch of the next symbol stays in flight across it, and the
 // workgroup barriers are raw s_barrier + lgkmcnt(0) (a __syncthreads()
 // would add vmcnt(0) and drain that prefetch).
@@ -69,7 +72,7 @@ __device__ __forceinline__ double2 mul_j(double2 a)
     return SIGN > 0 ? make_double2(-a.y, a.x) : make_double2(a.y, -a.x);
 }
 
-__device__ __forceinline__ int lds_pad(int e) { return e + (e >> 3); }
+__device__ __forceinline__ int lds_swz(int e) { return e ^ ((e >> 3) & 7); }
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS
 // operations, not for its vector-memory queue (so stores and LDS-DMA issued
@@ -95,7 +98,13 @@ __device__ __forceinline__ void load_twiddles(const double2* __restrict__ tw, do
                                               int nthreads)
 {
     constexpr int NHI = TwLds<LOGN>::NHI;
-    for (int i = t; i < NHI + 64; i += nthreads) lds_tw[i] = i < NHI ? tw[i * 64] : tw[i - NHI];
+    for (int i = t; i < NHI + 64; i += nthreads) {
+        const int j = i - NHI;
+        if (i < NHI)
+            lds_tw[i] = tw[i * 64];
+        else
+            lds_tw[NHI + (j ^ ((j >> 4) & 3))] = tw[j];
+    }
 }
 
 // W_N^j (forward sign) from the LDS table.
@@ -103,8 +112,10 @@ template <int LOGN>
 __device__ __forceinline__ double2 tw_get(const double2* __restrict__ lds_tw, int j)
 {
     constexpr int NHI = TwLds<LOGN>::NHI;
-    if constexpr (NHI == 1) return lds_tw[1 + j];
-    return cmul(lds_tw[j >> 6], lds_tw[NHI + (j & 63)]);
+    const int lo = j & 63;
+    const double2 wlo = lds_tw[NHI + (lo ^ ((lo >> 4) & 3))];
+    if constexpr (NHI == 1) return wlo;
+    return cmul(lds_tw[j >> 6], wlo);
 }
 
 // ---------------------------------------------------------------- DFTs
@@ -156,7 +167,7 @@ struct FftShape {
     static constexpr int T = N / 8;            // threads per transform
     static constexpr int NPASS8 = LOGN / 3;    // radix-8 passes
     static constexpr int REM = LOGN % 3;       // trailing radix-2/4 pass
-    static constexpr int PADN = N + N / 8;     // padded LDS elements
+    static constexpr int PADN = N;             // LDS elements per transform (swizzled, unpadded)
 };
 
 // One Stockham pass, radix R, input span NS. v[i] holds in[t + T*i].
@@ -197,7 +208,7 @@ __device__ __forceinline__ void stockham_pass(double2 (&v)[8], int t, const doub
             dft2<SIGN>(v[u], v[u + B]);
         const int idxD = (b - k) * R + k;
 #pragma unroll
-        for (int r = 0; r < R; ++r) lds[lds_pad(idxD + r * NS)] = v[u + r * B];
+        for (int r = 0; r < R; ++r) lds[lds_swz(idxD + r * NS)] = v[u + r * B];
     }
 }
 
@@ -206,7 +217,7 @@ __device__ __forceinline__ void lds_load8(double2 (&v)[8], int t, const double2*
 {
     constexpr int T = (1 << LOGN) / 8;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = lds[lds_pad(t + T * i)];
+    for (int i = 0; i < 8; ++i) v[i] = lds[lds_swz(t + T * i)];
 }
 
 // Remaining passes after the first one has been written to `lds`.
@@ -229,7 +240,7 @@ __device__ __forceinline__ void fft_tail(double2 (&v)[8], int t, const double2* 
 }
 
 // Full transform. On entry v[i] = x[t + T*i]; on exit the natural-order
-// result X[0..N) is in lds (padded indexing) and the workgroup is synced.
+// result X[0..N) is in lds (index lds_swz(k)) and the workgroup is synced.
 template <int LOGN, int SIGN>
 __device__ __forceinline__ void fft_block(double2 (&v)[8], int t, const double2* __restrict__ lds_tw,
                                           double2* __restrict__ lds)

@@ -196,7 +196,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) tx_kernel(TxArgs a)
         const unsigned long long g0 = a.sample_offset + (unsigned long long)sym * L;
         for (int j = t; j < L; j += T) {
             const int n = j < a.cp ? N - a.cp + j : j - a.cp;
-            double2 z = fft[lds_pad(n)];
+            double2 z = fft[lds_swz(n)];
             z.x *= a.inv_sqrt_n;
             z.y *= a.inv_sqrt_n;
             if (out16) {
@@ -311,12 +311,12 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
         lds_barrier();  // stage fully read: refill it with symbol s+1
         if (s + 1 < S) dma_symbol<LOGN>(x + (long)(s + 1) * L, stage, t);
         fft_block<LOGN, -1>(v, t, lds_tw, fft);
-        if (t < P) pil[s * P + t] = fft[lds_pad(pbin)];
+        if (t < P) pil[s * P + t] = fft[lds_swz(pbin)];
         if constexpr (STAGED) {
 #pragma unroll
             for (int i = 0; i < RX_DPT; ++i) {
                 const int d = t + T * i;
-                if (d < D) a.ystage[(f * S + s) * D + d] = fft[lds_pad(bins[i])];
+                if (d < D) a.ystage[(f * S + s) * D + d] = fft[lds_swz(bins[i])];
             }
         } else {
 #pragma unroll
@@ -324,7 +324,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
 #pragma unroll
                 for (int i = 0; i < RX_DPT; ++i) y[w][i] = y[w + 1][i];
 #pragma unroll
-            for (int i = 0; i < RX_DPT; ++i) y[SW - 1][i] = fft[lds_pad(bins[i])];
+            for (int i = 0; i < RX_DPT; ++i) y[SW - 1][i] = fft[lds_swz(bins[i])];
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
