@@ -20,6 +20,7 @@
 
 #include "../../include/ofdm_mi355x.h"
 #include "ofdm_internal.hpp"
+#include "ofdm_sync.hpp"
 
 using cd = std::complex<double>;
 
@@ -121,9 +122,18 @@ struct ofdm_ctx {
     double2* d_templ = nullptr;    // pr_sin_len
     double2* d_modpre = nullptr;   // D*npr
     double* d_t2mask = nullptr;    // t2 size
-    double2* d_t2tw = nullptr;     // t2-size twiddles (sync)
-    double2* d_prtw = nullptr;     // preamble-length twiddles (sync)
-    int sync_tables_ok = 0;
+    double2* d_t2tw = nullptr;     // t2-size twiddles (T2 detector)
+    int* d_first = nullptr;        // T2 detector min-block scratch
+    int t2_logn = -1;              // T2sin_size = 2^t2_logn, else -1 (detector unsupported)
+    struct CfoPlan {               // pilot_freq_sinh on a form of nsym symbols
+        int nsym = 0, logm = -1, g = 0;
+        double2* tw_sub = nullptr;
+        double2* tw_full = nullptr;
+        int* borders = nullptr;
+    };
+    std::vector<CfoPlan> cfo_plans;
+    double* d_cfo_scratch = nullptr;
+    size_t cfo_scratch_n = 0;
     // staged-rx scratch (grown on demand, only for num_symb > 8 or D > N/2)
     double2* d_scratch = nullptr;
     size_t scratch_bytes = 0;
@@ -262,9 +272,14 @@ int ofdm_destroy(ofdm_ctx* c)
     (void)hipSetDevice(c->device);
     void* ptrs[] = {c->d_tw, c->d_data_bin, c->d_data_slot, c->d_pilot_bin, c->d_bin_map, c->d_const,
                     c->d_const_bpsk, c->d_header, c->d_preamble, c->d_templ, c->d_modpre, c->d_t2mask,
-                    c->d_t2tw, c->d_prtw, c->d_scratch};
+                    c->d_t2tw, c->d_first, c->d_scratch, c->d_cfo_scratch};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
+    for (auto& pl : c->cfo_plans) {
+        if (pl.tw_sub) (void)hipFree(pl.tw_sub);
+        if (pl.tw_full) (void)hipFree(pl.tw_full);
+        if (pl.borders) (void)hipFree(pl.borders);
+    }
     delete c;
     return OFDM_OK;
 }
@@ -469,7 +484,57 @@ int ofdm_create(const ofdm_params* params, int device, ofdm_ctx** out)
             return rc;
         }
     }
+    // T2 detector tables
+    if (c->t2 >= 64 && c->t2 <= 4096 && ilog2_exact(c->t2) > 0) {
+        c->t2_logn = ilog2_exact(c->t2);
+        if ((rc = upload(&c->d_t2tw, twiddles(c->t2))) || (rc = upload(&c->d_first, std::vector<int>(1, 0)))) {
+            ofdm_destroy(c);
+            return rc;
+        }
+    }
     *out = c;
+    return OFDM_OK;
+}
+
+// pilot_freq_sinh plan for a form of nsym symbols: S = (N+cp)*nsym = M or 5*M,
+// M = 2^m; window borders exactly as Frame.hpp:311-321 computes them.
+static int cfo_plan(ofdm_ctx* c, int nsym, ofdm_ctx::CfoPlan** out)
+{
+    for (auto& pl : c->cfo_plans)
+        if (pl.nsym == nsym) {
+            *out = &pl;
+            return OFDM_OK;
+        }
+    const long S = (long)c->L * nsym;
+    ofdm_ctx::CfoPlan pl;
+    pl.nsym = nsym;
+    if (ilog2_exact(S) >= 6 && ilog2_exact(S) <= 12) {
+        pl.g = 1;
+        pl.logm = ilog2_exact(S);
+    } else if (S % 5 == 0 && ilog2_exact(S / 5) >= 6 && ilog2_exact(S / 5) <= 10) {
+        pl.g = 5;
+        pl.logm = ilog2_exact(S / 5);
+    } else {
+        return fail(OFDM_ERR_UNSUPPORTED, "pilot_freq_sinh: form length %ld is not 2^a or 5*2^a (64 <= 2^a <= %d)", S,
+                    4096);
+    }
+    const int P = c->P;
+    const double rel_bw = double(c->D + c->P) / (c->N);
+    const double rel_pilot_w = rel_bw / P;
+    const int pilot_w = int(S * rel_pilot_w);
+    std::vector<int> borders(P + 2);
+    for (int i = 0, j = int((1.0 - rel_bw - rel_pilot_w) / 2.0 * S); i < P + 2; i++) {
+        borders[i] = j;
+        j += pilot_w;
+    }
+    borders[0] = std::max(0, borders[0]);
+    for (int b : borders)
+        if (b < 0 || b > S) return fail(OFDM_ERR_UNSUPPORTED, "pilot_freq_sinh windows leave the spectrum");
+    int rc;
+    if ((rc = upload(&pl.tw_sub, twiddles(1 << pl.logm))) || (rc = upload(&pl.borders, borders))) return rc;
+    if (pl.g == 5 && (rc = upload(&pl.tw_full, twiddles((int)S)))) return rc;
+    c->cfo_plans.push_back(pl);
+    *out = &c->cfo_plans.back();
     return OFDM_OK;
 }
 
@@ -666,25 +731,177 @@ int ofdm_map(ofdm_ctx* c, const uint8_t* bytes, size_t nbytes, double* points_ou
     return OFDM_OK;
 }
 
-// ---- sync front end: implemented in ofdm_sync.hip (declared in ofdm_sync.hpp)
+// ---- sync front end (ofdm_sync.hip)
 int ofdm_t2_scan(ofdm_ctx* c, const double* iq, size_t n, long start, double* rel_out, int* first_out, void* stream)
 {
     if (!c || !iq) return fail(OFDM_ERR_INVALID, "null argument");
-    return fail(OFDM_ERR_UNSUPPORTED, "ofdm_t2_scan: not built yet");
+    if (c->t2_logn < 0) return fail(OFDM_ERR_UNSUPPORTED, "T2 detector needs T2sin_size = 2^a, 64..4096");
+    if (start < 0) return fail(OFDM_ERR_INVALID, "start < 0");
+    if (!aligned16(iq)) return fail(OFDM_ERR_INVALID, "iq must be 16-byte aligned");
+    ofdm::T2Args a{};
+    a.iq = reinterpret_cast<const double2*>(iq);
+    a.tw = c->d_t2tw;
+    a.start = start;
+    a.nblocks = (long)n > start ? ((long)n - start) / c->t2 : 0;
+    const int sm = (int)c->p.smooth, f1 = (int)c->p.t2_sin_f1, f2 = (int)c->p.t2_sin_f2;
+    a.a1 = std::max(0, f1 - sm);
+    a.b1 = std::min(c->t2 - 1, f1 + sm);
+    a.a2 = std::max(0, f2 - sm);
+    a.b2 = std::min(c->t2 - 1, f2 + sm);
+    a.level = (double)c->p.t2_sin_level / 1000;
+    a.rel_out = rel_out;
+    a.first_scratch = c->d_first;
+    hipError_t e = ofdm::launch_t2_scan(c->t2_logn, a, first_out, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "t2_scan launch");
+    return OFDM_OK;
 }
 
 int ofdm_find_preamble(ofdm_ctx* c, const double* iq, size_t n, const int* starts, size_t nstarts, int* idx_out,
                        void* stream)
 {
-    if (!c || !iq) return fail(OFDM_ERR_INVALID, "null argument");
-    return fail(OFDM_ERR_UNSUPPORTED, "ofdm_find_preamble: not built yet");
+    if (!c || !iq || (nstarts && (!starts || !idx_out))) return fail(OFDM_ERR_INVALID, "null argument");
+    if (!aligned16(iq)) return fail(OFDM_ERR_INVALID, "iq must be 16-byte aligned");
+    ofdm::PreambleArgs a{};
+    a.iq = reinterpret_cast<const double2*>(iq);
+    a.n = (long)n;
+    a.starts = starts;
+    a.nstarts = (long)nstarts;
+    a.idx_out = idx_out;
+    a.templ = c->d_templ;
+    a.L = (int)c->p.pr_sin_len;
+    a.cycles = (int)(2 * c->p.t2sin_size + c->p.pr_sin_len);
+    a.level = (double)c->p.pr_level / 1000;
+    hipError_t e = ofdm::launch_find_preamble(a, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "find_preamble launch");
+    return OFDM_OK;
 }
 
-int ofdm_sync_frames(ofdm_ctx* c, double* frames, size_t nframes, size_t frame_stride, int stages,
-                     const double* cfo_in, double* cfo_out, double* chan_out, void* stream)
+int ofdm_cfo_estimate(ofdm_ctx* c, const double* x, size_t nframes, size_t stride, int nsym, double* cfo_out,
+                      void* stream)
+{
+    if (!c || !x || !cfo_out) return fail(OFDM_ERR_INVALID, "null argument");
+    if (nsym < 1 || stride < (size_t)c->L * nsym) return fail(OFDM_ERR_INVALID, "bad nsym / frame_stride");
+    if (!aligned16(x)) return fail(OFDM_ERR_INVALID, "x must be 16-byte aligned");
+    if (nframes == 0) return OFDM_OK;
+    ofdm_ctx::CfoPlan* pl = nullptr;
+    int rc = cfo_plan(c, nsym, &pl);
+    if (rc) return rc;
+    ofdm::CfoArgs a{};
+    a.x = reinterpret_cast<const double2*>(x);
+    a.nframes = (long)nframes;
+    a.frame_stride = (long)stride;
+    a.tw_sub = pl->tw_sub;
+    a.tw_full = pl->tw_full;
+    a.borders = pl->borders;
+    a.P = c->P;
+    a.cfo_out = cfo_out;
+    hipError_t e = ofdm::launch_cfo(pl->logm, pl->g, a, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "cfo launch");
+    return OFDM_OK;
+}
+
+int ofdm_freq_shift(ofdm_ctx* c, double* x, size_t nframes, size_t stride, size_t nsamples, const double* cfo,
+                    void* stream)
+{
+    if (!c || !x || !cfo) return fail(OFDM_ERR_INVALID, "null argument");
+    if (nframes > 1 && stride < nsamples) return fail(OFDM_ERR_INVALID, "frame_stride < nsamples");
+    if (!aligned16(x)) return fail(OFDM_ERR_INVALID, "x must be 16-byte aligned");
+    ofdm::ShiftArgs a{reinterpret_cast<double2*>(x), (long)nframes, (long)stride, (long)nsamples, cfo};
+    hipError_t e = ofdm::launch_freq_shift(a, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "freq_shift launch");
+    return OFDM_OK;
+}
+
+int ofdm_cp_sync(ofdm_ctx* c, double* x, size_t nframes, size_t stride, int nsym, void* stream)
+{
+    if (!c || !x) return fail(OFDM_ERR_INVALID, "null argument");
+    if (nsym < 1 || nsym > 64 || (nframes > 1 && stride < (size_t)c->L * nsym))
+        return fail(OFDM_ERR_INVALID, "bad nsym / frame_stride");
+    if (!aligned16(x)) return fail(OFDM_ERR_INVALID, "x must be 16-byte aligned");
+    ofdm::CpArgs a{reinterpret_cast<double2*>(x), (long)nframes, (long)stride, nsym, c->N, c->cp};
+    hipError_t e = ofdm::launch_cp_sync(a, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "cp_sync launch");
+    return OFDM_OK;
+}
+
+int ofdm_phase_sync(ofdm_ctx* c, double* x, size_t nframes, size_t stride, size_t nsamples, const double* pr,
+                    size_t pr_len, void* stream)
+{
+    if (!c || !x) return fail(OFDM_ERR_INVALID, "null argument");
+    if (!pr) {
+        pr = reinterpret_cast<const double*>(c->d_preamble);
+        pr_len = (size_t)c->geo.preamble_len;
+    }
+    if (pr_len > nsamples && nframes > 1 && stride < pr_len) return fail(OFDM_ERR_INVALID, "pr_len exceeds the form");
+    if (!aligned16(x) || !aligned16(pr)) return fail(OFDM_ERR_INVALID, "buffers must be 16-byte aligned");
+    ofdm::PhaseArgs a{reinterpret_cast<double2*>(x), (long)nframes, (long)stride, (long)nsamples,
+                      reinterpret_cast<const double2*>(pr), (long)pr_len};
+    hipError_t e = ofdm::launch_phase_sync(a, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "phase_sync launch");
+    return OFDM_OK;
+}
+
+int ofdm_chan_estimate(ofdm_ctx* c, const double* x, size_t nframes, size_t stride, double* chan_out,
+                       size_t chan_stride, void* stream)
+{
+    if (!c || !x || !chan_out) return fail(OFDM_ERR_INVALID, "null argument");
+    if (!aligned16(x) || !aligned16(chan_out)) return fail(OFDM_ERR_INVALID, "buffers must be 16-byte aligned");
+    if (c->P > c->N / 8) return fail(OFDM_ERR_UNSUPPORTED, "num_pilot_subc > fft_size/8");
+    ofdm::ChanArgs a{};
+    a.tab = c->tables(true);
+    a.x = reinterpret_cast<const double2*>(x);
+    a.nframes = (long)nframes;
+    a.frame_stride = (long)stride;
+    a.mod_pre = c->d_modpre;
+    a.chan_out = reinterpret_cast<double2*>(chan_out);
+    a.chan_stride = (long)chan_stride;
+    a.npr = c->npr;
+    a.D = c->D;
+    a.P = c->P;
+    a.cp = c->cp;
+    a.pilot_ampl = (double)c->p.pilot_ampl / 1000;
+    hipError_t e = ofdm::launch_chan(c->logn, a, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "chan launch");
+    return OFDM_OK;
+}
+
+int ofdm_sync_frames(ofdm_ctx* c, double* frames, size_t nframes, size_t stride, int stages, const double* cfo_in,
+                     double* cfo_out, double* chan_out, void* stream)
 {
     if (!c || !frames) return fail(OFDM_ERR_INVALID, "null argument");
-    return fail(OFDM_ERR_UNSUPPORTED, "ofdm_sync_frames: not built yet");
+    const int nsym = c->npr + c->S;
+    const size_t nsamples = (size_t)c->L * nsym;
+    if (nframes > 1 && stride < nsamples) return fail(OFDM_ERR_INVALID, "frame_stride < preamble+message");
+    if (nframes == 0) return OFDM_OK;
+    const double* cfo = cfo_in;
+    int rc;
+    if (stages & OFDM_SYNC_CFO) {
+        double* dst = cfo_out;
+        if (!dst) {
+            if (c->cfo_scratch_n < nframes) {
+                HIP_TRY(hipSetDevice(c->device));
+                if (c->d_cfo_scratch) HIP_TRY(hipFree(c->d_cfo_scratch));
+                c->d_cfo_scratch = nullptr;
+                c->cfo_scratch_n = 0;
+                HIP_TRY(hipMalloc((void**)&c->d_cfo_scratch, nframes * sizeof(double)));
+                c->cfo_scratch_n = nframes;
+            }
+            dst = c->d_cfo_scratch;
+        }
+        if ((rc = ofdm_cfo_estimate(c, frames, nframes, stride, c->npr, dst, stream))) return rc;
+        cfo = dst;
+    }
+    if (stages & OFDM_SYNC_FREQ_SHIFT) {
+        if (!cfo) return fail(OFDM_ERR_INVALID, "freq shift without a CFO (set OFDM_SYNC_CFO or pass cfo_in)");
+        if ((rc = ofdm_freq_shift(c, frames, nframes, stride, nsamples, cfo, stream))) return rc;
+    }
+    if ((stages & OFDM_SYNC_CP) && (rc = ofdm_cp_sync(c, frames, nframes, stride, nsym, stream))) return rc;
+    if ((stages & OFDM_SYNC_PHASE) && (rc = ofdm_phase_sync(c, frames, nframes, stride, nsamples, nullptr, 0, stream)))
+        return rc;
+    if ((stages & OFDM_SYNC_CHAN) && chan_out &&
+        (rc = ofdm_chan_estimate(c, frames, nframes, stride, chan_out, (size_t)c->D, stream)))
+        return rc;
+    return OFDM_OK;
 }
 
 }  // extern "C"

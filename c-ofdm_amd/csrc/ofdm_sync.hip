@@ -1,0 +1,600 @@
+// ofdm_sync.hip — the rx synchronisation front end as HIP kernels for gfx950
+// (SURVEY.md §8f rank 1). One kernel per reference member, batched over
+// frames (a located frame = one workgroup or one grid row):
+//
+//   t2_scan_kernel        T2SIN_FORM::find_t2sin / corr   (Frame.hpp:96-197)
+//   find_preamble_kernel  PREAMBLE_FORM::find_preamble    (Frame.cpp:338-378)
+//   cfo_kernel            OFDM_FORM::pilot_freq_sinh      (Frame.hpp:285-337)
+//   freq_shift_kernel     OFDM_FORM::freq_shift           (Frame.hpp:340-348)
+//   cp_sync_kernel        OFDM_FORM::cp_freq_sinh         (Frame.hpp:238-263)
+//   phase_sync_kernel     OFDM_FORM::pr_phase_sinh        (Frame.hpp:265-274)
+//   chan_kernel           PREAMBLE_FORM::chan_char_lq     (Frame.hpp:389-434)
+//
+// Arithmetic notes. The reference builds its phasor ramps by recursive
+// products (p *= step); here every sample's phasor is computed directly
+// (sincospi / sincos of the accumulated angle), which is within ~1e-13 of the
+// recursion (whose own rounding drift is of that order) and needs no serial
+// chain. The preamble detector keeps the reference's serial running-energy
+// recurrence and its exact j = 0..L-1 accumulation order (no FMA), so its
+// threshold decisions are bit-identical.
+#include <hip/hip_runtime.h>
+#include <climits>
+#include <cstdint>
+
+#include "ofdm_fft.hpp"
+#include "ofdm_sync.hpp"
+
+namespace ofdm {
+
+namespace {
+
+__device__ __forceinline__ double2 cconj_mul(double2 a, double2 b)  // conj(a) * b, as g++ (no FMA)
+{
+    return cmul_exact(make_double2(a.x, -a.y), b);
+}
+
+__device__ __forceinline__ double2 cadd_rn(double2 a, double2 b)
+{
+    return make_double2(__dadd_rn(a.x, b.x), __dadd_rn(a.y, b.y));
+}
+
+// Block-wide complex / double sums (NT threads, multiple of 64 or < 64).
+template <int NT>
+__device__ __forceinline__ double2 block_sum2(double2 v, double2* red)
+{
+    constexpr int W0 = NT >= 64 ? 32 : NT / 2;
+#pragma unroll
+    for (int o = W0; o > 0; o >>= 1) {
+        v.x += __shfl_xor(v.x, o);
+        v.y += __shfl_xor(v.y, o);
+    }
+    constexpr int NW = (NT + 63) / 64;
+    if constexpr (NW == 1) {
+        return v;
+    } else {
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        __syncthreads();
+        if (lane == 0) red[w] = v;
+        __syncthreads();
+        double2 s = make_double2(0.0, 0.0);
+#pragma unroll
+        for (int i = 0; i < NW; ++i) s = cadd(s, red[i]);
+        return s;
+    }
+}
+
+constexpr int SYNC_THREADS = 256;
+
+}  // namespace
+
+// ========================================================================
+// T2 detector: G transforms of N = 2^LOGN points per workgroup.
+// ========================================================================
+template <int LOGN>
+struct T2Geo {
+    static constexpr int N = 1 << LOGN;
+    static constexpr int T = N / 8;
+    static constexpr int G = T >= 256 ? 1 : 256 / T;  // blocks per workgroup
+    static constexpr int NT = G * T;
+};
+
+template <int LOGN>
+__global__ void __launch_bounds__(T2Geo<LOGN>::NT) t2_scan_kernel(T2Args a)
+{
+    using Geo = T2Geo<LOGN>;
+    constexpr int N = Geo::N, T = Geo::T, G = Geo::G;
+    extern __shared__ double2 smem[];
+    double2* lds_tw = smem;
+    double2* red = lds_tw + TwLds<LOGN>::SIZE;  // G * (T/64 + 1) * 2 doubles
+    double2* fftb = red + 2 * G * (T / 64 + 1);
+    const int tid = threadIdx.x, g = tid / T, t = tid - g * T;
+    load_twiddles<LOGN>(a.tw, lds_tw, tid, Geo::NT);
+    const long b = (long)blockIdx.x * G + g;
+    const bool live = b < a.nblocks;
+    const double2* x = a.iq + a.start + (live ? b : 0) * N;
+    double2 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = live ? x[t + T * i] : make_double2(0.0, 0.0);
+    __syncthreads();
+    fft_block<LOGN, -1>(v, t, lds_tw, fftb + g * N);
+    // energies: total = sum |X|^2, sin = sum mask*|X|^2 (Frame.hpp:172-180)
+    double tot = 0.0, sine = 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int k = t + T * i;
+        const double2 z = fftb[g * N + lds_swz(k)];
+        const double e = z.x * z.x + z.y * z.y;
+        const double m = (double)((k >= a.a1 && k <= a.b1) + (k >= a.a2 && k <= a.b2));
+        tot += e;
+        sine += m * e;
+    }
+    // reduce within the group (T lanes: a wave fragment, or T/64 waves)
+    constexpr int W0 = T >= 64 ? 32 : T / 2;
+#pragma unroll
+    for (int o = W0; o > 0; o >>= 1) {
+        tot += __shfl_xor(tot, o);
+        sine += __shfl_xor(sine, o);
+    }
+    if constexpr (T > 64) {
+        constexpr int NW = T / 64;
+        if ((tid & 63) == 0) red[g * NW + (t >> 6)] = make_double2(tot, sine);
+        __syncthreads();
+        tot = 0.0;
+        sine = 0.0;
+        for (int w = 0; w < NW; ++w) {
+            tot += red[g * NW + w].x;
+            sine += red[g * NW + w].y;
+        }
+    }
+    if (t == 0 && live) {
+        double out = 0.0;
+        if (tot != 0.0) {
+            const double rel = sine / tot;
+            if (!isnan(rel) && rel > a.level) {
+                out = rel;
+                atomicMin(a.first_scratch, (int)b);
+            }
+        }
+        if (a.rel_out) a.rel_out[b] = out;
+    }
+}
+
+__global__ void t2_finalize_kernel(const int* scratch, int* first_out, long start, int size)
+{
+    const int m = *scratch;
+    *first_out = m == INT_MAX ? -1 : (int)(start + (long)m * size);
+}
+
+template <int LOGN>
+static hipError_t t2_launch_n(const T2Args& a, hipStream_t st)
+{
+    using Geo = T2Geo<LOGN>;
+    const size_t shm = sizeof(double2) * (TwLds<LOGN>::SIZE + 2 * Geo::G * (Geo::T / 64 + 1) + Geo::G * Geo::N);
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)t2_scan_kernel<LOGN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        attr = true;
+    }
+    const long grid = (a.nblocks + Geo::G - 1) / Geo::G;
+    hipLaunchKernelGGL(t2_scan_kernel<LOGN>, dim3((unsigned)grid), dim3(Geo::NT), shm, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_t2_scan(int logn, const T2Args& a, int* first_out, hipStream_t st)
+{
+    if (a.first_scratch) {
+        const int big = INT_MAX;
+        hipError_t e = hipMemsetD32Async((hipDeviceptr_t)a.first_scratch, big, 1, st);
+        if (e != hipSuccess) return e;
+    }
+    hipError_t e = hipSuccess;
+    if (a.nblocks > 0) {
+        switch (logn) {
+            case 6: e = t2_launch_n<6>(a, st); break;
+            case 7: e = t2_launch_n<7>(a, st); break;
+            case 8: e = t2_launch_n<8>(a, st); break;
+            case 9: e = t2_launch_n<9>(a, st); break;
+            case 10: e = t2_launch_n<10>(a, st); break;
+            case 11: e = t2_launch_n<11>(a, st); break;
+            case 12: e = t2_launch_n<12>(a, st); break;
+            default: return hipErrorInvalidValue;
+        }
+    }
+    if (e != hipSuccess) return e;
+    if (first_out) {
+        hipLaunchKernelGGL(t2_finalize_kernel, dim3(1), dim3(1), 0, st, a.first_scratch, first_out, a.start,
+                           1 << logn);
+        e = hipGetLastError();
+    }
+    return e;
+}
+
+// ========================================================================
+// Preamble detector: one workgroup per start index.
+// ========================================================================
+__global__ void __launch_bounds__(SYNC_THREADS) find_preamble_kernel(PreambleArgs a)
+{
+    extern __shared__ double2 smem[];
+    const int L = a.L, C = a.cycles;
+    double2* xs = smem;                      // C + L samples
+    double2* c = xs + C + L;                 // L template taps
+    double* normv = reinterpret_cast<double*>(c + L);  // C running energies
+    int* best = reinterpret_cast<int*>(normv + C);
+    const int t = threadIdx.x;
+    const long s = a.starts[blockIdx.x];
+    for (int i = t; i < C + L; i += SYNC_THREADS) {
+        const long j = s + i;
+        xs[i] = (j >= 0 && j < a.n) ? a.iq[j] : make_double2(0.0, 0.0);
+    }
+    for (int i = t; i < L; i += SYNC_THREADS) c[i] = a.templ[i];
+    if (t == 0) *best = INT_MAX;
+    __syncthreads();
+    // serial running energy, exactly the reference's operation order (Frame.cpp:346-375)
+    if (t == 0) {
+        double norm = 0.0;
+        for (int i = 0; i < L; ++i) norm = __dadd_rn(norm, __dadd_rn(__dmul_rn(xs[i].x, xs[i].x), __dmul_rn(xs[i].y, xs[i].y)));
+        for (int i = 0; i < C; ++i) {
+            normv[i] = norm;
+            const double2 p = xs[i + L], q = xs[i];
+            norm = __dadd_rn(norm, __dadd_rn(__dmul_rn(p.x, p.x), __dmul_rn(p.y, p.y)));
+            norm = __dsub_rn(norm, __dadd_rn(__dmul_rn(q.x, q.x), __dmul_rn(q.y, q.y)));
+        }
+    }
+    // correlation per lag, j = 0..L-1 in order (Frame.cpp:360-363)
+    double2 en[4];
+    int nl = 0;
+    for (int i = t; i < C && nl < 4; i += SYNC_THREADS, ++nl) {
+        double2 e = make_double2(0.0, 0.0);
+        for (int j = 0; j < L; ++j) e = cadd_rn(e, cmul_exact(xs[i + j], c[j]));
+        en[nl] = e;
+    }
+    __syncthreads();
+    nl = 0;
+    for (int i = t; i < C && nl < 4; i += SYNC_THREADS, ++nl) {
+        const double norm = normv[i];
+        if (norm > 1.0 && hypot(en[nl].x, en[nl].y) / sqrt(norm) > a.level) atomicMin(best, i);
+    }
+    // lags beyond 4*SYNC_THREADS (C > 1024): continue serially in chunks
+    for (int base = 4 * SYNC_THREADS; base < C; base += SYNC_THREADS) {
+        const int i = base + t;
+        if (i < C) {
+            double2 e = make_double2(0.0, 0.0);
+            for (int j = 0; j < L; ++j) e = cadd_rn(e, cmul_exact(xs[i + j], c[j]));
+            const double norm = normv[i];
+            if (norm > 1.0 && hypot(e.x, e.y) / sqrt(norm) > a.level) atomicMin(best, i);
+        }
+    }
+    __syncthreads();
+    if (t == 0) a.idx_out[blockIdx.x] = *best == INT_MAX ? -10 : (int)(s + *best);
+}
+
+hipError_t launch_find_preamble(const PreambleArgs& a, hipStream_t st)
+{
+    if (a.nstarts <= 0) return hipSuccess;
+    const size_t shm = sizeof(double2) * (a.cycles + 2 * (size_t)a.L) + sizeof(double) * a.cycles + 16;
+    if (shm > 160 * 1024) return hipErrorInvalidValue;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)find_preamble_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL(find_preamble_kernel, dim3((unsigned)a.nstarts), dim3(SYNC_THREADS), shm, st, a);
+    return hipGetLastError();
+}
+
+// ========================================================================
+// pilot_freq_sinh: FFT of the whole form (M or 5*M points, M = 2^LOGM) as G
+// interleaved sub-FFTs of M points + a radix-5 combine, |.|, fftshift, first
+// argmax per pilot window.
+// ========================================================================
+template <int LOGM, int G>
+__global__ void __launch_bounds__(G * (1 << LOGM) / 8) cfo_kernel(CfoArgs a)
+{
+    constexpr int M = 1 << LOGM, T = M / 8, NT = G * T, S = G * M;
+    extern __shared__ double2 smem[];
+    double2* lds_tw = smem;
+    double2* fftb = lds_tw + TwLds<LOGM>::SIZE;          // G * M
+    double* amp = reinterpret_cast<double*>(fftb + S);    // S magnitudes (fftshifted)
+    int* wsum = reinterpret_cast<int*>(amp + S);          // per-window argmax
+    const int tid = threadIdx.x, g = tid / T, t = tid - g * T;
+    const long f = blockIdx.x;
+    const double2* x = a.x + f * a.frame_stride;
+    load_twiddles<LOGM>(a.tw_sub, lds_tw, tid, NT);
+    double2 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = x[(long)G * (t + T * i) + g];  // decimated input x[G*n + g]
+    __syncthreads();
+    fft_block<LOGM, -1>(v, t, lds_tw, fftb + g * M);
+    // X[k + M*r] = sum_q W_S^{q k} W_G^{q r} F_q[k]; amp stored fftshifted:
+    // shifted[i] = spec[(i + S/2) % S]  (Frame.hpp:300-305)
+    const int half = S / 2;
+    for (int k = tid; k < M; k += NT) {
+        if constexpr (G == 1) {
+            const double2 z = fftb[lds_swz(k)];
+            amp[(k + half) % S] = hypot(z.x, z.y);
+        } else {
+            double2 tq[G];
+#pragma unroll
+            for (int q = 0; q < G; ++q) {
+                const double2 fq = fftb[q * M + lds_swz(k)];
+                tq[q] = q == 0 ? fq : cmul(fq, a.tw_full[(long)q * k % S]);
+            }
+#pragma unroll
+            for (int r = 0; r < G; ++r) {
+                double2 acc = tq[0];
+#pragma unroll
+                for (int q = 1; q < G; ++q) acc = cadd(acc, cmul(tq[q], a.tw_full[(long)((q * r) % G) * M]));
+                const int idx = k + M * r;
+                amp[(idx + half) % S] = hypot(acc.x, acc.y);
+            }
+        }
+    }
+    __syncthreads();
+    // first argmax inside each pilot window [borders[i], borders[i+1]), i != P/2
+    // (std::max_element: strictly-greater keeps the first maximum); one
+    // thread per window, windows are ~41 bins wide.
+    for (int i = tid; i <= a.P; i += NT) {
+        const int lo = a.borders[i], hi = a.borders[i + 1];
+        int bi = hi;  // max_element of an empty range = end
+        if (lo < hi) {
+            bi = lo;
+            double bv = amp[lo];
+            for (int j = lo + 1; j < hi; ++j)
+                if (bv < amp[j]) {
+                    bv = amp[j];
+                    bi = j;
+                }
+        }
+        wsum[i] = bi;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double shift = 0.0;
+        for (int i = 0; i <= a.P; ++i)
+            if (i != a.P / 2) shift += wsum[i];
+        shift /= a.P;
+        shift -= S / 2;
+        shift /= S;
+        a.cfo_out[f] = shift;
+    }
+}
+
+template <int LOGM, int G>
+static hipError_t cfo_launch_n(const CfoArgs& a, hipStream_t st)
+{
+    constexpr int M = 1 << LOGM, NT = G * M / 8;
+    static_assert(NT <= 1024, "cfo workgroup too large");
+    const size_t shm = sizeof(double2) * (TwLds<LOGM>::SIZE + (size_t)G * M) + sizeof(double) * G * M +
+                       sizeof(int) * (a.P + 2) + 16;
+    if (shm > 160 * 1024) return hipErrorInvalidValue;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)cfo_kernel<LOGM, G>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL((cfo_kernel<LOGM, G>), dim3((unsigned)a.nframes), dim3(NT), shm, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_cfo(int logm, int g, const CfoArgs& a, hipStream_t st)
+{
+    if (a.nframes <= 0) return hipSuccess;
+    if (g == 1) {
+        switch (logm) {
+            case 6: return cfo_launch_n<6, 1>(a, st);
+            case 7: return cfo_launch_n<7, 1>(a, st);
+            case 8: return cfo_launch_n<8, 1>(a, st);
+            case 9: return cfo_launch_n<9, 1>(a, st);
+            case 10: return cfo_launch_n<10, 1>(a, st);
+            case 11: return cfo_launch_n<11, 1>(a, st);
+            case 12: return cfo_launch_n<12, 1>(a, st);
+            default: return hipErrorInvalidValue;
+        }
+    }
+    if (g == 5) {
+        switch (logm) {
+            case 6: return cfo_launch_n<6, 5>(a, st);
+            case 7: return cfo_launch_n<7, 5>(a, st);
+            case 8: return cfo_launch_n<8, 5>(a, st);
+            case 9: return cfo_launch_n<9, 5>(a, st);
+            case 10: return cfo_launch_n<10, 5>(a, st);
+            default: return hipErrorInvalidValue;
+        }
+    }
+    return hipErrorInvalidValue;
+}
+
+// ========================================================================
+// freq_shift: x[n] *= exp(-2 pi i cfo n)
+// ========================================================================
+__global__ void __launch_bounds__(SYNC_THREADS) freq_shift_kernel(ShiftArgs a)
+{
+    const long f = blockIdx.y;
+    const double cfo = a.cfo[f];
+    double2* x = a.x + f * a.frame_stride;
+    for (long n = blockIdx.x * (long)SYNC_THREADS + threadIdx.x; n < a.nsamples;
+         n += (long)gridDim.x * SYNC_THREADS) {
+        double sn, cs;
+        sincospi(-2.0 * cfo * (double)n, &sn, &cs);
+        x[n] = cmul(x[n], make_double2(cs, sn));
+    }
+}
+
+hipError_t launch_freq_shift(const ShiftArgs& a, hipStream_t st)
+{
+    if (a.nframes <= 0 || a.nsamples <= 0) return hipSuccess;
+    long gx = (a.nsamples + SYNC_THREADS * 4 - 1) / (SYNC_THREADS * 4);
+    if (gx > 64) gx = 64;
+    hipLaunchKernelGGL(freq_shift_kernel, dim3((unsigned)gx, (unsigned)a.nframes), dim3(SYNC_THREADS), 0, st, a);
+    return hipGetLastError();
+}
+
+// ========================================================================
+// cp_freq_sinh: phi_s = arg sum_{j<cp} conj(x[sL+j]) x[sL+j+N];
+// sample (s, j) *= exp(-i (sum_{q<s} phi_q * L + phi_s * j) / N)
+// ========================================================================
+__global__ void __launch_bounds__(SYNC_THREADS) cp_sync_kernel(CpArgs a)
+{
+    __shared__ double2 red[SYNC_THREADS / 64];
+    __shared__ double phi[64];
+    const long f = blockIdx.x;
+    double2* x = a.x + f * a.frame_stride;
+    const int t = threadIdx.x, L = a.N + a.cp;
+    for (int s = 0; s < a.nsym; ++s) {
+        double2 acc = make_double2(0.0, 0.0);
+        for (int j = t; j < a.cp; j += SYNC_THREADS) acc = cadd(acc, cconj_mul(x[(long)s * L + j], x[(long)s * L + j + a.N]));
+        acc = block_sum2<SYNC_THREADS>(acc, red);
+        if (t == 0) phi[s] = atan2(acc.y, acc.x);
+        __syncthreads();
+    }
+    const long total = (long)a.nsym * L;
+    for (long n = t; n < total; n += SYNC_THREADS) {
+        const int s = (int)(n / L), j = (int)(n - (long)s * L);
+        double psi = 0.0;
+        for (int q = 0; q < s; ++q) psi += phi[q];
+        const double th = -(psi * L + phi[s] * j) / a.N;
+        double sn, cs;
+        sincos(th, &sn, &cs);
+        x[n] = cmul(x[n], make_double2(cs, sn));
+    }
+}
+
+hipError_t launch_cp_sync(const CpArgs& a, hipStream_t st)
+{
+    if (a.nframes <= 0) return hipSuccess;
+    if (a.nsym > 64) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(cp_sync_kernel, dim3((unsigned)a.nframes), dim3(SYNC_THREADS), 0, st, a);
+    return hipGetLastError();
+}
+
+// ========================================================================
+// pr_phase_sinh: phi = arg sum_i conj(pr_i) x_i; x *= exp(-i phi)
+// ========================================================================
+__global__ void __launch_bounds__(SYNC_THREADS) phase_sync_kernel(PhaseArgs a)
+{
+    __shared__ double2 red[SYNC_THREADS / 64];
+    __shared__ double2 rot;
+    const long f = blockIdx.x;
+    double2* x = a.x + f * a.frame_stride;
+    const int t = threadIdx.x;
+    double2 acc = make_double2(0.0, 0.0);
+    for (long i = t; i < a.pr_len; i += SYNC_THREADS) acc = cadd(acc, cconj_mul(a.pr[i], x[i]));
+    acc = block_sum2<SYNC_THREADS>(acc, red);
+    if (t == 0) {
+        double sn, cs;
+        sincos(-atan2(acc.y, acc.x), &sn, &cs);
+        rot = make_double2(cs, sn);
+    }
+    __syncthreads();
+    const double2 r = rot;
+    for (long n = t; n < a.nsamples; n += SYNC_THREADS) x[n] = cmul(x[n], r);
+}
+
+hipError_t launch_phase_sync(const PhaseArgs& a, hipStream_t st)
+{
+    if (a.nframes <= 0) return hipSuccess;
+    hipLaunchKernelGGL(phase_sync_kernel, dim3((unsigned)a.nframes), dim3(SYNC_THREADS), 0, st, a);
+    return hipGetLastError();
+}
+
+// ========================================================================
+// chan_char_lq: FFT_FORM::read of the preamble form (phys over its pilots,
+// coef = F0/F0), phase of pr/mod_preamble over the first D/2 carriers,
+// one-pass unwrap, least squares on raw sums, unit phasors.
+// ========================================================================
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 8) chan_kernel(ChanArgs a)
+{
+    using FS = FftShape<LOGN>;
+    constexpr int N = FS::N, T = FS::T;
+    extern __shared__ double2 smem[];
+    double2* lds_tw = smem;
+    double2* fftb = lds_tw + TwLds<LOGN>::SIZE;   // N
+    double2* pil = fftb + N;                       // npr * P
+    double2* dat = pil + a.npr * a.P;              // D/2 raw bins of symbol 0
+    double* ph = reinterpret_cast<double*>(dat + a.D / 2 + 1);
+    double* red = ph + a.D / 2 + 2;
+    const int t = threadIdx.x;
+    const long f = blockIdx.x;
+    const double2* x = a.x + f * a.frame_stride;
+    const int L = N + a.cp, half = a.D / 2;
+    load_twiddles<LOGN>(a.tab.tw, lds_tw, t, T);
+    __syncthreads();
+    for (int s = 0; s < a.npr; ++s) {
+        double2 v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = x[(long)s * L + a.cp + t + T * i];
+        fft_block<LOGN, -1>(v, t, lds_tw, fftb);
+        for (int j = t; j < a.P; j += T) pil[s * a.P + j] = fftb[lds_swz(a.tab.pilot_bin[j])];
+        if (s == 0)
+            for (int i = t; i < half; i += T) dat[i] = fftb[lds_swz(a.tab.data_bin[i])];
+        __syncthreads();
+    }
+    // phys (Frame.cpp:76-80), parallel sum
+    double acc = 0.0;
+    for (int i = t; i < a.npr * a.P; i += T) acc += hypot(pil[i].x, pil[i].y);
+    {
+        double2 r2 = block_sum2<T>(make_double2(acc, 0.0), reinterpret_cast<double2*>(red));
+        acc = r2.x;
+    }
+    const double phys = acc / ((double)(a.P * a.npr) * a.pilot_ampl);
+    // pr[i] = (F/phys) / coef, coef = (F[0,p]/phys)/(F[0,p]/phys); phase of pr/mod
+    for (int i = t; i < half; i += T) {
+        const int j = a.tab.data_slot[i];
+        const double2 p0 = make_double2(pil[j].x / phys, pil[j].y / phys);
+        const double2 coef = cdiv_exact(p0, p0);
+        const double2 fs = make_double2(dat[i].x / phys, dat[i].y / phys);
+        const double2 q = cdiv_exact(cdiv_exact(fs, coef), a.mod_pre[i]);
+        ph[i] = atan2(q.y, q.x);
+    }
+    __syncthreads();
+    if (t == 0) {  // one-pass unwrap against the already-adjusted previous value (Frame.hpp:407-414)
+        for (int i = 1; i < half; ++i) {
+            const double d = ph[i] - ph[i - 1];
+            if (d > M_PI)
+                ph[i] -= 2 * M_PI;
+            else if (d < -M_PI)
+                ph[i] += 2 * M_PI;
+        }
+    }
+    __syncthreads();
+    double sxy = 0.0, sy = 0.0;
+    for (int i = t; i < half; i += T) {
+        sxy += ph[i] * i;
+        sy += ph[i];
+    }
+    const double2 sums = block_sum2<T>(make_double2(sxy, sy), reinterpret_cast<double2*>(red) + 16);
+    // integer sums are exact in any order
+    const double hn = (double)half;
+    const double sx = hn * (hn - 1) / 2, sx2 = (hn - 1) * hn * (2 * hn - 1) / 6;
+    const double b = (sums.x - sx * sums.y) / (sx2 - sx * sx);
+    const double aa = sums.y - b * sx;
+    double2* chan = a.chan_out + f * a.chan_stride;
+    for (int i = t; i < a.D; i += T) {
+        double th;
+        if (i < half)
+            th = __dadd_rn(__dmul_rn(b, (double)i), aa);
+        else
+            th = __dadd_rn(__dadd_rn(__dmul_rn(-b, (double)a.D) / 2, __dmul_rn((double)(i - half), b)), aa);
+        double sn, cs;
+        sincos(th, &sn, &cs);
+        chan[i] = make_double2(cs, sn);
+    }
+}
+
+template <int LOGN>
+static hipError_t chan_launch_n(const ChanArgs& a, hipStream_t st)
+{
+    using FS = FftShape<LOGN>;
+    const size_t shm = sizeof(double2) * (TwLds<LOGN>::SIZE + FS::N + (size_t)a.npr * a.P + a.D / 2 + 1) +
+                       sizeof(double) * (a.D / 2 + 2) + sizeof(double2) * 40;
+    if (shm > 160 * 1024) return hipErrorInvalidValue;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)chan_kernel<LOGN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL(chan_kernel<LOGN>, dim3((unsigned)a.nframes), dim3(FS::T), shm, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_chan(int logn, const ChanArgs& a, hipStream_t st)
+{
+    if (a.nframes <= 0) return hipSuccess;
+    switch (logn) {
+        case 6: return chan_launch_n<6>(a, st);
+        case 7: return chan_launch_n<7>(a, st);
+        case 8: return chan_launch_n<8>(a, st);
+        case 9: return chan_launch_n<9>(a, st);
+        case 10: return chan_launch_n<10>(a, st);
+        case 11: return chan_launch_n<11>(a, st);
+        case 12: return chan_launch_n<12>(a, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace ofdm

@@ -1,0 +1,81 @@
+// ofdm_sync.hpp — argument blocks and launchers of the rx sync front end
+// (ofdm_sync.hip), called from ofdm_capi.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "ofdm_internal.hpp"
+
+namespace ofdm {
+
+struct T2Args {
+    const double2* iq;      // stream
+    const double2* tw;      // T2sin_size forward twiddles
+    long start;             // first sample scanned
+    long nblocks;           // floor((n - start) / size)
+    int a1, b1, a2, b2;     // detector mask bands (Frame.cpp:120-133)
+    double level;           // T2_sin_level / 1000
+    double* rel_out;        // nullable: nblocks ratios (0 where <= level)
+    int* first_scratch;     // device int, min block index above level
+};
+
+struct PreambleArgs {
+    const double2* iq;
+    long n;
+    const int* starts;
+    long nstarts;
+    int* idx_out;
+    const double2* templ;   // pr_sin_len conj template
+    int L;                  // pr_sin_len
+    int cycles;             // 2*T2sin_size + pr_sin_len
+    double level;           // pr_level / 1000
+};
+
+struct CfoArgs {
+    const double2* x;
+    long nframes, frame_stride;
+    const double2* tw_sub;   // M-point forward twiddles
+    const double2* tw_full;  // S-point forward twiddles (G == 5)
+    const int* borders;      // P + 2 window borders (Frame.hpp:311-321)
+    int P;
+    double* cfo_out;
+};
+
+struct ShiftArgs {
+    double2* x;
+    long nframes, frame_stride, nsamples;
+    const double* cfo;
+};
+
+struct CpArgs {
+    double2* x;
+    long nframes, frame_stride;
+    int nsym, N, cp;
+};
+
+struct PhaseArgs {
+    double2* x;
+    long nframes, frame_stride, nsamples;
+    const double2* pr;
+    long pr_len;
+};
+
+struct ChanArgs {
+    DevTables tab;
+    const double2* x;           // preamble form
+    long nframes, frame_stride;
+    const double2* mod_pre;     // D*npr BPSK points
+    double2* chan_out;
+    long chan_stride;
+    int npr, D, P, cp;
+    double pilot_ampl;
+};
+
+hipError_t launch_t2_scan(int logn, const T2Args& a, int* first_out, hipStream_t st);
+hipError_t launch_find_preamble(const PreambleArgs& a, hipStream_t st);
+hipError_t launch_cfo(int logm, int g, const CfoArgs& a, hipStream_t st);
+hipError_t launch_freq_shift(const ShiftArgs& a, hipStream_t st);
+hipError_t launch_cp_sync(const CpArgs& a, hipStream_t st);
+hipError_t launch_phase_sync(const PhaseArgs& a, hipStream_t st);
+hipError_t launch_chan(int logn, const ChanArgs& a, hipStream_t st);
+
+}  // namespace ofdm

@@ -86,6 +86,11 @@ SIGNATURES = {
     "ofdm_map": (_I, [_V, _V, _SZ, _V, _V]),
     "ofdm_t2_scan": (_I, [_V, _V, _SZ, _L, _V, _V, _V]),
     "ofdm_find_preamble": (_I, [_V, _V, _SZ, _V, _SZ, _V, _V]),
+    "ofdm_cfo_estimate": (_I, [_V, _V, _SZ, _SZ, _I, _V, _V]),
+    "ofdm_freq_shift": (_I, [_V, _V, _SZ, _SZ, _SZ, _V, _V]),
+    "ofdm_cp_sync": (_I, [_V, _V, _SZ, _SZ, _I, _V]),
+    "ofdm_phase_sync": (_I, [_V, _V, _SZ, _SZ, _SZ, _V, _SZ, _V]),
+    "ofdm_chan_estimate": (_I, [_V, _V, _SZ, _SZ, _V, _SZ, _V]),
     "ofdm_sync_frames": (_I, [_V, _V, _SZ, _SZ, _I, _V, _V, _V, _V]),
 }
 
@@ -225,6 +230,28 @@ class Modem:
 
     def find_preamble(self, iq, n: int, starts, nstarts: int, idx_out, stream=None):
         check(lib().ofdm_find_preamble(self.h, _ptr(iq), n, _ptr(starts), nstarts, _ptr(idx_out),
+                                       _stream(stream)))
+
+    def cfo_estimate(self, x, nframes: int, frame_stride: int, nsym: int, cfo_out, stream=None):
+        check(lib().ofdm_cfo_estimate(self.h, _ptr(x), nframes, frame_stride, nsym, _ptr(cfo_out),
+                                      _stream(stream)))
+
+    def freq_shift(self, x, nframes: int, frame_stride: int, nsamples: int, cfo, stream=None):
+        check(lib().ofdm_freq_shift(self.h, _ptr(x), nframes, frame_stride, nsamples, _ptr(cfo),
+                                    _stream(stream)))
+
+    def cp_sync(self, x, nframes: int, frame_stride: int, nsym: int, stream=None):
+        check(lib().ofdm_cp_sync(self.h, _ptr(x), nframes, frame_stride, nsym, _stream(stream)))
+
+    def phase_sync(self, x, nframes: int, frame_stride: int, nsamples: int, pr=None, pr_len: int = 0,
+                   stream=None):
+        check(lib().ofdm_phase_sync(self.h, _ptr(x), nframes, frame_stride, nsamples, _ptr(pr), pr_len,
+                                    _stream(stream)))
+
+    def chan_estimate(self, x, nframes: int, frame_stride: int, chan_out, chan_stride: int | None = None,
+                      stream=None):
+        cs = self.params.num_data_subc if chan_stride is None else chan_stride
+        check(lib().ofdm_chan_estimate(self.h, _ptr(x), nframes, frame_stride, _ptr(chan_out), cs,
                                        _stream(stream)))
 
     def sync_frames(self, frames, nframes: int, frame_stride: int, stages: int = SYNC_ALL,

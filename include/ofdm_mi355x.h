@@ -184,27 +184,58 @@ int ofdm_t2_scan(ofdm_ctx* ctx, const double* iq, size_t n, long start,
                  double* rel_out, int* first_out, void* stream);
 
 /* PREAMBLE_FORM::find_preamble (Frame.cpp:338-378) for a batch of starts:
- * idx_out[i] = first lag index (start_i + lag) whose normalised
- * correlation exceeds pr_level/1000, or -10. Device arrays. */
+ * idx_out[i] = starts[i] + first lag whose normalised correlation with the
+ * preamble template exceeds pr_level/1000 (lags 0 .. 2*T2sin_size+pr_sin_len-1,
+ * running window energy updated after each test, as the reference), or -10.
+ * Samples past n read as 0. Device arrays. Callers add +1 (main.cpp:53). */
 int ofdm_find_preamble(ofdm_ctx* ctx, const double* iq, size_t n,
                        const int* starts, size_t nstarts, int* idx_out, void* stream);
 
-/* Per-frame synchronisation of a located frame, in place on the
- * message_with_preamble region (preamble + message, (N+cp)*(num_pr_symb+num_symb)
- * samples at frames + f*frame_stride):
- *   cfo = OFDM_FORM::pilot_freq_sinh   (Frame.hpp:285-337)  -> cfo_out[f]
- *   OFDM_FORM::freq_shift(cfo)         (Frame.hpp:340-348)
- *   OFDM_FORM::cp_freq_sinh            (Frame.hpp:238-263)
- *   OFDM_FORM::pr_phase_sinh(ofdm_preamble) (Frame.hpp:265-274)
- *   PREAMBLE_FORM::chan_char_lq        (Frame.hpp:389-434) -> chan_out[f*D]
- * Any of `stages` bits may be cleared to skip a stage (OFDM_SYNC_* below). */
+/* ---- per-frame synchronisation, batched over located frames ------------
+ * `x` points at the first sample of a form in frame 0; frame f's form starts
+ * at x + 2*f*frame_stride. A "form" is nsym consecutive [CP|body] symbols
+ * (OFDM_FORM: preamble form nsym = num_pr_symb, message_with_preamble form
+ * nsym = num_pr_symb + num_symb). All pointers are device pointers. */
+
+/* OFDM_FORM::pilot_freq_sinh (Frame.hpp:285-337): coarse CFO (cycles/sample)
+ * of each frame's form from the pilot peaks of its (N+cp)*nsym-point FFT.
+ * Needs (N+cp)*nsym = 2^a or 5*2^a. */
+int ofdm_cfo_estimate(ofdm_ctx* ctx, const double* x, size_t nframes, size_t frame_stride,
+                      int nsym, double* cfo_out, void* stream);
+
+/* OFDM_FORM::freq_shift (Frame.hpp:340-348): x[n] *= exp(-2*pi*i*cfo[f]*n),
+ * n = 0 .. nsamples-1, in place. cfo: device array of nframes values. */
+int ofdm_freq_shift(ofdm_ctx* ctx, double* x, size_t nframes, size_t frame_stride,
+                    size_t nsamples, const double* cfo, void* stream);
+
+/* OFDM_FORM::cp_freq_sinh (Frame.hpp:238-263): per-symbol CP-correlation fine
+ * CFO, phase-continuous across the nsym symbols of the form, in place. */
+int ofdm_cp_sync(ofdm_ctx* ctx, double* x, size_t nframes, size_t frame_stride, int nsym,
+                 void* stream);
+
+/* OFDM_FORM::pr_phase_sinh (Frame.hpp:265-274): common phase vs pr[0..pr_len)
+ * (device), applied to nsamples samples in place. pr = NULL uses the
+ * context's own ofdm_preamble (preamble_len samples), as main.cpp:63 does. */
+int ofdm_phase_sync(ofdm_ctx* ctx, double* x, size_t nframes, size_t frame_stride,
+                    size_t nsamples, const double* pr, size_t pr_len, void* stream);
+
+/* PREAMBLE_FORM::chan_char_lq (Frame.hpp:389-434): linear-phase channel
+ * estimate from the preamble form at x -> chan_out[f*D .. f*D+D) unit phasors
+ * (data/phases.bin layout). chan_stride: complex elements between frames. */
+int ofdm_chan_estimate(ofdm_ctx* ctx, const double* x, size_t nframes, size_t frame_stride,
+                       double* chan_out, size_t chan_stride, void* stream);
+
+/* The main.cpp:60-66 chain on each frame's message_with_preamble region
+ * (preamble + message, in place): cfo -> freq_shift -> cp_sync -> phase_sync
+ * (context preamble) -> chan_estimate. Clear OFDM_SYNC_* bits to skip a stage
+ * (cfo_in, nullable, then supplies the CFO). Outputs nullable. */
 enum {
     OFDM_SYNC_CFO = 1, OFDM_SYNC_FREQ_SHIFT = 2, OFDM_SYNC_CP = 4,
     OFDM_SYNC_PHASE = 8, OFDM_SYNC_CHAN = 16, OFDM_SYNC_ALL = 31
 };
 int ofdm_sync_frames(ofdm_ctx* ctx, double* frames, size_t nframes, size_t frame_stride,
-                     int stages, const double* cfo_in /* nullable: used when CFO stage is off */,
-                     double* cfo_out, double* chan_out, void* stream);
+                     int stages, const double* cfo_in, double* cfo_out, double* chan_out,
+                     void* stream);
 
 #ifdef __cplusplus
 }

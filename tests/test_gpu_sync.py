@@ -1,0 +1,157 @@
+"""GPU parity of the rx synchronisation front end against
+the oracle and the reference's golden capture (data/data.bin, t2_sin_corr.bin,
+phases.bin, constell.bin, data.txt): one test per reference member, then the
+fused main.cpp:51-80 chain, then batches of synthetic impaired frames."""
+import numpy as np
+import pytest
+
+import oracle as O
+from common import B, CC, D, G, golden, payload, rel_err
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import ofdm_mi355x as M  # noqa: E402
+
+_m = {}
+
+
+def modem(cfg):
+    key = repr(sorted(cfg.items()))
+    if key not in _m:
+        _m[key] = M.Modem(cfg, 0)
+    return _m[key]
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+GD = golden()
+GEO = O.geometry(G)
+
+
+def test_t2_scan_matches_golden_corr_and_find():
+    m = modem(G)
+    x = GD["data"]
+    dx = dev(x)
+    nb = len(x) // G["t2sin_size"]
+    rel = torch.full((nb,), -1.0, dtype=torch.float64, device="cuda")
+    first = torch.zeros((1,), dtype=torch.int32, device="cuda")
+    m.t2_scan(dx, len(x), 0, rel_out=rel, first_out=first)
+    assert np.abs(host(rel) - GD["t2_corr"]).max() < 1e-12          # T2SIN_FORM::corr == t2_sin_corr.bin
+    assert int(host(first)[0]) == GD["t2_first_block_start"]         # find_t2sin(buf, 0)
+    # from an arbitrary start (rx.cpp scans from pos), and a start with no marker left
+    for start in (1, 5000, 11040, 19302 - 300, 30000):
+        m.t2_scan(dx, len(x), start, first_out=first)
+        assert int(host(first)[0]) == O.find_t2sin(G, x, start), start
+
+
+def test_find_preamble_matches_reference_indices():
+    m = modem(G)
+    x = GD["data"]
+    starts = np.array([10752, 10752 + 256, 0, 19000, 30000, len(x) - 100], np.int32)
+    out = torch.zeros((len(starts),), dtype=torch.int32, device="cuda")
+    m.find_preamble(dev(x), len(x), dev(starts), len(starts), out)
+    got = host(out)
+    want = [O.find_preamble(G, x, int(s)) for s in starts]
+    assert list(got) == want
+    assert got[0] + 1 == GD["preamble_begin"][0]
+
+
+def _golden_mwp():
+    pr = GD["preamble_begin"][0]
+    return GD["data"][pr: pr + GEO["preamble_len"] + GEO["message_len"]].copy()
+
+
+def test_stagewise_sync_matches_oracle_on_golden_frame():
+    m = modem(G)
+    mwp = _golden_mwp()
+    pre, modp, _ = O.preamble_setup(G)
+    n = len(mwp)
+    x = dev(mwp)
+    cfo = torch.zeros((1,), dtype=torch.float64, device="cuda")
+    m.cfo_estimate(x, 1, n, G["num_pr_symb"], cfo)
+    assert float(host(cfo)[0]) == GD["cfo_frame1"]  # exact: integer bin arithmetic
+    ref = O.freq_shift(mwp, GD["cfo_frame1"])
+    m.freq_shift(x, 1, n, n, cfo)
+    assert rel_err(host(x), ref) < 1e-11
+    ref = O.cp_freq_sinh(G, ref)
+    m.cp_sync(x, 1, n, G["num_pr_symb"] + G["num_symb"])
+    assert rel_err(host(x), ref) < 1e-10
+    ref = O.pr_phase_sinh(ref, pre)
+    m.phase_sync(x, 1, n, n)
+    assert rel_err(host(x), ref) < 1e-10
+    chan = torch.zeros((G["num_data_subc"],), dtype=torch.complex128, device="cuda")
+    m.chan_estimate(x, 1, n, chan)
+    assert np.abs(host(chan) - GD["phases"]).max() < 1e-10           # data/phases.bin
+
+
+def test_fused_sync_and_demod_reproduce_golden_constellation():
+    m = modem(G)
+    x = dev(_golden_mwp())
+    n = x.numel()
+    chan = torch.zeros((G["num_data_subc"],), dtype=torch.complex128, device="cuda")
+    cfo = torch.zeros((1,), dtype=torch.float64, device="cuda")
+    m.sync_frames(x, 1, n, M.SYNC_ALL, cfo_out=cfo, chan_out=chan)
+    cons = torch.zeros((GEO["npts"],), dtype=torch.complex128, device="cuda")
+    out = torch.zeros((GEO["bytes_per_frame"],), dtype=torch.uint8, device="cuda")
+    msg = x[GEO["preamble_len"]:]
+    m.rx(msg, 1, chan=chan, constell_out=cons, bytes_out=out)
+    assert float(host(cfo)[0]) == GD["cfo_frame1"]
+    assert np.abs(host(cons) - GD["constell"]).max() / np.abs(GD["constell"]).max() < 1e-9  # constell.bin
+    assert np.array_equal(host(out), GD["payload"])                   # data.txt (+ MAC header)
+
+
+def _impaired_frames(cfg, nf, seed, cfo_max=0.002, snr_db=25.0):
+    """tx frames (T2+preamble+message) with per-frame CFO, phase and AWGN."""
+    g = O.geometry(cfg)
+    rng = np.random.default_rng(seed)
+    data = payload(nf * g["bytes_per_frame"], seed)
+    frames = []
+    for f in range(nf):
+        fr = O.frame_write(cfg, data[f * g["bytes_per_frame"]:(f + 1) * g["bytes_per_frame"]])
+        n = np.arange(len(fr))
+        cfo = rng.uniform(-cfo_max, cfo_max)
+        fr = fr * np.exp(2j * np.pi * cfo * n + 1j * rng.uniform(-np.pi, np.pi))
+        frames.append(O.awgn(fr, 10 ** (-snr_db / 20), seed=seed * 100 + f))
+    return np.concatenate(frames), data
+
+
+@pytest.mark.parametrize("name,cfg", [("D", D), ("B", B), ("C", CC)])
+def test_batched_sync_chain_matches_oracle(name, cfg):
+    m = modem(cfg)
+    g = O.geometry(cfg)
+    nf = 4
+    stream, data = _impaired_frames(cfg, nf, seed=11 + len(name))
+    L = g["frame_len"]
+    t2 = cfg["t2sin_size"]
+    pre, modp, _ = O.preamble_setup(cfg)
+    # GPU: sync every frame's message_with_preamble region in place (stride = frame)
+    x = dev(stream)
+    mwp = x[t2:]
+    cfo = torch.zeros((nf,), dtype=torch.float64, device="cuda")
+    chan = torch.zeros((nf * cfg["num_data_subc"],), dtype=torch.complex128, device="cuda")
+    m.sync_frames(mwp, nf, L, M.SYNC_ALL, cfo_out=cfo, chan_out=chan)
+    out = torch.zeros((nf * g["bytes_per_frame"],), dtype=torch.uint8, device="cuda")
+    cons = torch.zeros((nf * g["npts"],), dtype=torch.complex128, device="cuda")
+    m.rx(mwp[g["preamble_len"]:], nf, frame_stride=L, chan=chan, chan_stride=cfg["num_data_subc"],
+         constell_out=cons, bytes_out=out)
+    hcfo, hchan, hcons, hout, hx = host(cfo), host(chan), host(cons), host(out), host(x)
+    for f in range(nf):
+        r = stream[f * L + t2: f * L + L].copy()
+        c = O.pilot_freq_sinh(cfg, r[: g["preamble_len"]])
+        assert hcfo[f] == c
+        r = O.pr_phase_sinh(O.cp_freq_sinh(cfg, O.freq_shift(r, c)), pre)
+        assert rel_err(hx[f * L + t2: f * L + L], r) < 1e-9
+        ch = O.chan_char_lq(cfg, r[: g["preamble_len"]], modp)
+        assert rel_err(hchan[f * cfg["num_data_subc"]:(f + 1) * cfg["num_data_subc"]], ch) < 1e-9
+        oc = O.ofdm_fft(cfg, r[g["preamble_len"]:]) / np.tile(ch, cfg["num_symb"])
+        ob, _ = O.demod(cfg["mod_type"], oc)
+        assert rel_err(hcons[f * g["npts"]:(f + 1) * g["npts"]], oc) < 1e-9
+        assert np.array_equal(hout[f * g["bytes_per_frame"]:(f + 1) * g["bytes_per_frame"]], ob)
