@@ -62,6 +62,17 @@ def load_pmc(workload: str):
     return best
 
 
+def payload_bytes(begin: int, count: int, seed: int = 0x5EED) -> np.ndarray:
+    """Counter-based synthetic payload: byte i of the whole job = splitmix64(seed + i) & 0xFF,
+    so every rank generates exactly its shard and the job is independent of the GPU count."""
+    z = np.arange(begin, begin + count, dtype=np.uint64) + np.uint64(seed)
+    z = z * np.uint64(0x9E3779B97F4A7C15)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    z = z ^ (z >> np.uint64(31))
+    return (z & np.uint64(0xFF)).astype(np.uint8)
+
+
 def cpu_baseline(p, data_host: np.ndarray, nframes_sample: int, noise_std: float, budget_s: float):
     """Oracle (plain-C restatement) tx+AWGN+rx loopback on host cores, 1 thread,
     on a bounded sample of the same workload. Reported beside the GPU number."""
@@ -92,18 +103,19 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames", type=int, default=8192, help="frames per GPU (8 symbols each)")
+    ap.add_argument("--frames", type=int, default=8192, help="frames per GPU (8 symbols each); weak scaling")
+    ap.add_argument("--total-frames", type=int, default=0,
+                    help="strong scaling: shard this many frames over the GPUs (config 5: 30517 = 10 GB)")
     ap.add_argument("--snr-db", type=float, default=10.0)
     ap.add_argument("--cpu-budget", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
     import torch
+    import ofdm_dist
     import ofdm_mi355x as M
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = ofdm_dist.env_world()
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -116,15 +128,18 @@ def main():
     p = dict(CONFIG_B)
     modem = M.Modem(p, local)
     geo = modem.geo
-    nf = args.frames
+    strong = args.total_frames > 0
+    if strong:
+        f0, nf = ofdm_dist.shard(args.total_frames, world, rank)
+    else:
+        f0, nf = rank * args.frames, args.frames
     S = p["num_symb"]
     msg = geo.message_len
     bpf = geo.bytes_per_frame
     npts = p["num_data_subc"] * S
 
-    # payload: seeded per rank (independent shards), resident in HBM
-    rng = np.random.default_rng(0x5EED + rank)
-    data_host = rng.integers(0, 256, nf * bpf, dtype=np.uint8)
+    # payload: this rank's shard of the job's counter-based payload, resident in HBM
+    data_host = payload_bytes(f0 * bpf, nf * bpf)
     data = torch.from_numpy(data_host).to(dev)
     iq = torch.empty((nf * msg,), dtype=torch.complex128, device=dev)
     cons = torch.empty((nf * npts,), dtype=torch.complex128, device=dev)
@@ -141,7 +156,7 @@ def main():
     def step(i, events=None):
         if events:
             events[0].record(stream)
-        modem.tx(data, nf, iq, noise_std=noise_std, seed=1, sample_offset=rank * nf * msg, stream=stream)
+        modem.tx(data, nf, iq, noise_std=noise_std, seed=1, sample_offset=f0 * msg, stream=stream)
         if events:
             events[1].record(stream)
         modem.rx(iq, nf, constell_out=cons, bytes_out=out, ref=data, bit_errors=errs, stream=stream)
@@ -155,23 +170,19 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     errs.zero_()
+    consts = torch.tensor([K * nf * bpf * 8, K * nf * msg, K * nf], dtype=torch.int64, device=dev)
+    torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(K):
         step(i, ev[i])
     # final BER/throughput reduction (the one collective of the path)
-    totals = torch.stack([errs[0], torch.tensor(K * nf * bpf * 8, device=dev),
-                          torch.tensor(K * nf * msg, device=dev), torch.tensor(K * nf, device=dev)])
-    if dist:
-        dist.all_reduce(totals)
+    totals = torch.cat([errs, consts])
+    ofdm_dist.reduce_counters(totals, dist)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    el_t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if dist:
-        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
-    elapsed = float(el_t.item())
+    elapsed = ofdm_dist.max_over_ranks(time.perf_counter() - t0, dev, dist)
 
     tx_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
     rx_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
@@ -182,7 +193,8 @@ def main():
     rx_bytes = nf * S * rx_bytes_per_symbol(p)
     tx_bytes = nf * S * tx_bytes_per_symbol(p)
     achieved = rx_bytes / (rx_ms * 1e-3) / 1e9
-    workload = f"config2_B_N2048_D1024_P32_cp512_QPSK_{nf}frames_x8sym_per_gpu"
+    workload = (f"config5_B_N2048_D1024_P32_cp512_QPSK_{args.total_frames}frames_sharded" if strong else
+                f"config2_B_N2048_D1024_P32_cp512_QPSK_{nf}frames_x8sym_per_gpu")
     pmc = load_pmc(workload)
 
     result = {
@@ -194,7 +206,7 @@ def main():
         "warmup": W,
         "ms_per_step": elapsed / K * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": f"synthetic: seeded random payload per rank, counter-based AWGN Es/N0={args.snr_db:g} dB",
@@ -203,6 +215,7 @@ def main():
             "fft_size": p["fft_size"], "num_data_subc": p["num_data_subc"],
             "num_pilot_subc": p["num_pilot_subc"], "cp_size": p["cp_size"], "num_symb": S,
             "mod_type": p["mod_type"], "frames_per_gpu": nf, "symbols_per_gpu": nf * S,
+            "total_frames": args.total_frames if strong else world * nf,
             "samples_per_step_per_gpu": nf * msg, "parallelism": f"frame-sharded x{world}",
         },
         "roofline": {
@@ -216,8 +229,8 @@ def main():
             "avg_launch_ms": rx_ms,
             "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
         },
-        "rx_iq_samples_per_s": world * nf * msg / (rx_ms * 1e-3),
-        "tx_iq_samples_per_s": world * nf * msg / (tx_ms * 1e-3),
+        "rx_iq_samples_per_s_per_gpu": nf * msg / (rx_ms * 1e-3),
+        "tx_iq_samples_per_s_per_gpu": nf * msg / (tx_ms * 1e-3),
         "tx_achieved_gbs": tx_bytes / (tx_ms * 1e-3) / 1e9,
         "tx_avg_launch_ms": tx_ms,
         "ber": float(tot[0]) / max(float(tot[1]), 1.0),

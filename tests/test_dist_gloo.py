@@ -1,0 +1,82 @@
+"""Multi-rank driver logic on CPU (gloo, world_size 2): frame sharding covers
+the batch exactly once, the per-rank results concatenate to the single-rank
+result, and the one SUM all-reduce of the counters equals the serial totals.
+The per-rank compute here is the oracle (CPU checker); on MI355X bench.py runs
+the HIP kernels with the same sharding and reduction (c-ofdm_amd/python/ofdm_dist.py)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import ofdm_dist
+import oracle as O
+from common import D
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+
+def test_shard_partitions_exactly():
+    for n in (0, 1, 7, 8, 30517, 65536):
+        for w in (1, 2, 3, 4, 8):
+            seen = []
+            for r in range(w):
+                b, c = ofdm_dist.shard(n, w, r)
+                seen.extend(range(b, b + c))
+            assert seen == list(range(n))
+            counts = [ofdm_dist.shard(n, w, r)[1] for r in range(w)]
+            assert max(counts) - min(counts) <= 1
+
+
+NF = 10
+
+
+def _dataset():
+    g = O.geometry(D)
+    data = np.random.default_rng(5).integers(0, 256, NF * g["bytes_per_frame"], dtype=np.uint8)
+    iq = O.awgn(O.tx_batch(D, data, NF), 0.45, seed=7)
+    return g, data, iq
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g, data, iq = _dataset()
+    b, c = ofdm_dist.shard(NF, world, rank)
+    L, bpf = g["message_len"], g["bytes_per_frame"]
+    _, out, errs = O.rx_batch(D, iq[b * L:(b + c) * L], c, L, ref=data[b * bpf:(b + c) * bpf])
+    counters = torch.tensor([errs, c * bpf * 8, c * L, c], dtype=torch.int64)
+    ofdm_dist.reduce_counters(counters, dist)
+    parts = [None] * world
+    dist.all_gather_object(parts, (b, out))
+    if rank == 0:
+        q.put((counters.tolist(), parts))
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_rank_shard_and_reduce_equals_single_rank():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    counters, parts = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    g, data, iq = _dataset()
+    _, out, errs = O.rx_batch(D, iq, NF, g["message_len"], ref=data)
+    assert counters == [errs, NF * g["bytes_per_frame"] * 8, NF * g["message_len"], NF]
+    joined = np.concatenate([o for _, o in sorted(parts, key=lambda t: t[0])])
+    assert np.array_equal(joined, out)
