@@ -731,6 +731,67 @@ int ofdm_map(ofdm_ctx* c, const uint8_t* bytes, size_t nbytes, double* points_ou
     return OFDM_OK;
 }
 
+int ofdm_fft_write(ofdm_ctx* c, const double* points, size_t nframes, double* fft_buf, void* stream)
+{
+    if (!c || !points || !fft_buf) return fail(OFDM_ERR_INVALID, "null argument");
+    if (!aligned16(points) || !aligned16(fft_buf)) return fail(OFDM_ERR_INVALID, "buffers must be 16-byte aligned");
+    if (nframes == 0) return OFDM_OK;
+    ofdm::TxArgs a{};
+    fill_tx(c, a, nullptr, nframes, fft_buf, (size_t)c->N * c->S, nullptr, nullptr);
+    a.points = reinterpret_cast<const double2*>(points);
+    a.cp = 0;  // FFT_buf holds bodies only
+    hipError_t e = ofdm::launch_tx(c->logn, a, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "fft_write launch");
+    return OFDM_OK;
+}
+
+int ofdm_fft_read(ofdm_ctx* c, const double* fft_buf, size_t nframes, double* restored, void* stream)
+{
+    if (!c || !fft_buf || !restored) return fail(OFDM_ERR_INVALID, "null argument");
+    if (!aligned16(fft_buf) || !aligned16(restored)) return fail(OFDM_ERR_INVALID, "buffers must be 16-byte aligned");
+    if (nframes == 0) return OFDM_OK;
+    ofdm::RxArgs a{};
+    a.tab = c->tables(false);
+    a.iq = reinterpret_cast<const double2*>(fft_buf);
+    a.nframes = (long)nframes;
+    a.frame_stride = (long)c->N * c->S;
+    a.constell = reinterpret_cast<double2*>(restored);
+    a.S = c->S;
+    a.D = c->D;
+    a.P = c->P;
+    a.seg = c->seg;
+    a.cp = 0;  // no CP in FFT_buf
+    a.k = c->k;
+    a.bytes_per_frame = c->geo.bytes_per_frame;
+    a.pilot_ampl = (double)c->p.pilot_ampl / 1000;
+    if (!(c->S <= ofdm::RX_SMAX && c->D <= ofdm::RX_DPT * (c->N / 8))) a.ystage = a.constell;
+    hipError_t e = ofdm::launch_rx(c->logn, a, (hipStream_t)stream, nullptr);
+    if (e != hipSuccess) return hip_fail(e, "fft_read launch");
+    return OFDM_OK;
+}
+
+int ofdm_bit_convert(ofdm_ctx* c, const uint8_t* in, size_t len, int in_bits, int out_bits, uint8_t* out,
+                     size_t* out_len, void* stream)
+{
+    if (!c || (len && (!in || !out))) return fail(OFDM_ERR_INVALID, "null argument");
+    if (in_bits < 1 || in_bits > 8 || out_bits < 1 || out_bits > 8) return fail(OFDM_ERR_INVALID, "bits must be 1..8");
+    const size_t total = len * (size_t)in_bits;
+    const size_t n = total / out_bits + (total % out_bits > 0);
+    if (out_len) *out_len = n;
+    hipError_t e = ofdm::launch_bit_convert(in, (long)len, in_bits, out_bits, out, (long)n, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "bit_convert launch");
+    return OFDM_OK;
+}
+
+int ofdm_int16_to_double(ofdm_ctx* c, const int16_t* in, size_t n, double* out, void* stream)
+{
+    if (!c || (n && (!in || !out))) return fail(OFDM_ERR_INVALID, "null argument");
+    if (((uintptr_t)in & 3) || !aligned16(out)) return fail(OFDM_ERR_INVALID, "misaligned buffers");
+    hipError_t e = ofdm::launch_i16_to_f64(in, (long)n, out, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "int16_to_double launch");
+    return OFDM_OK;
+}
+
 // ---- sync front end (ofdm_sync.hip)
 int ofdm_t2_scan(ofdm_ctx* c, const double* iq, size_t n, long start, double* rel_out, int* first_out, void* stream)
 {

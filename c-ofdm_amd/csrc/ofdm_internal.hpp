@@ -19,6 +19,7 @@ struct DevTables {
 struct TxArgs {
     DevTables tab;
     const uint8_t* bytes;       // nframes * bytes_per_frame
+    const double2* points;      // nullable: mapped points instead of bytes (FFT_FORM::write)
     double2* iq;                // frame f message at iq + f*frame_stride (+ msg_offset)
     int16_t* iq16;              // nullable, same indexing, 2 x int16 per sample
     const double2* header;      // T2+preamble samples (nullable: message only)
@@ -60,6 +61,9 @@ hipError_t launch_rx(int logn, const RxArgs& a, hipStream_t stream, bool* staged
 hipError_t launch_demap(double2* pts, long n, int k, uint8_t* bytes, hipStream_t stream);
 hipError_t launch_map(const uint8_t* bytes, long nbytes, int k, const double2* table, double2* out,
                       hipStream_t stream);
+hipError_t launch_bit_convert(const uint8_t* in, long len, int in_bits, int out_bits, uint8_t* out, long out_len,
+                              hipStream_t stream);
+hipError_t launch_i16_to_f64(const int16_t* in, long n, double* out, hipStream_t stream);
 
 // Register-resident rx limits: S*ceil(D/T) <= RX_REG_SLOTS.
 constexpr int RX_SMAX = 8;

@@ -124,7 +124,8 @@ __device__ __forceinline__ unsigned long long block_sum_u64(unsigned long long v
 // thread's bin classification are loaded once per workgroup, and the next
 // symbol's payload bytes are fetched into registers while this one is
 // transformed and written.
-template <int LOGN>
+// POINTS = true: FFT_FORM::write on given constellation points (no payload bytes).
+template <int LOGN, bool POINTS>
 __global__ void __launch_bounds__((1 << LOGN) / 8) tx_kernel(TxArgs a)
 {
     using FS = FftShape<LOGN>;
@@ -158,7 +159,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) tx_kernel(TxArgs a)
     // iteration, so the loads' latency hides behind the FFT.
     uint8_t nb[8];
     long sym = blockIdx.x;
-    if (sym < nsym) {
+    if (!POINTS && sym < nsym) {
         const uint8_t* src = sym_bytes(sym);
 #pragma unroll
         for (int r = 0; r < 8; ++r)
@@ -173,7 +174,9 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) tx_kernel(TxArgs a)
         double2 v[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            if (kind[i] >= 0) {
+            if (POINTS && kind[i] >= 0) {
+                v[i] = a.points[sym * a.D + kind[i]];
+            } else if (kind[i] >= 0) {
                 const int bit = kind[i] * k;
                 const int byte = bit >> 3, off = bit & 7;
                 const int w = ((int)sbytes[byte] << 8) | (off + k > 8 ? (int)sbytes[byte + 1] : 0);
@@ -183,9 +186,11 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) tx_kernel(TxArgs a)
             }
         }
         const long nxt = sym + gridDim.x;
-        const uint8_t* nsrc = sym_bytes(nxt < nsym ? nxt : sym);
+        if constexpr (!POINTS) {
+            const uint8_t* nsrc = sym_bytes(nxt < nsym ? nxt : sym);
 #pragma unroll
-        for (int r = 0; r < 8; ++r) nb[r] = nsrc[t + T * r < bps ? t + T * r : 0];
+            for (int r = 0; r < 8; ++r) nb[r] = nsrc[t + T * r < bps ? t + T * r : 0];
+        }
 
         fft_block<LOGN, +1>(v, t, lds_tw, fft);
 
@@ -223,9 +228,11 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) tx_kernel(TxArgs a)
                 }
             }
         }
+        if constexpr (!POINTS) {
 #pragma unroll
-        for (int r = 0; r < 8; ++r)
-            if (t + T * r < bps) sbytes[t + T * r] = nb[r];
+            for (int r = 0; r < 8; ++r)
+                if (t + T * r < bps) sbytes[t + T * r] = nb[r];
+        }
         lds_barrier();  // next payload visible; fft[] output reads precede the next pass 0
     }
 }
@@ -452,37 +459,73 @@ __global__ void map_kernel(const uint8_t* bytes, long nbytes, int k, const doubl
     out[g] = table[symbol_bits(bytes, nbytes, g, k)];
 }
 
+// Modulation::bit_stream_converter: output unit o = bits [o*ob, (o+1)*ob) of
+// the MSB-first stream of ib-bit input units (zero past the end).
+__global__ void bit_convert_kernel(const uint8_t* in, long len, int ib, int ob, uint8_t* out, long out_len)
+{
+    const long o = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (o >= out_len) return;
+    const long total = len * ib;
+    int v = 0;
+    for (int b = 0; b < ob; ++b) {
+        const long bit = o * ob + b;
+        int x = 0;
+        if (bit < total) {
+            const long u = bit / ib;
+            x = (in[u] >> (ib - 1 - (int)(bit - u * ib))) & 1;
+        }
+        v = (v << 1) | x;
+    }
+    out[o] = (uint8_t)v;
+}
+
+// FRAME_FORM::form_int16_to_double: element-wise int16 -> f64 (16 B out per 4 B in).
+__global__ void i16_to_f64_kernel(const short2* __restrict__ in, long n, double2* __restrict__ out)
+{
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const short2 v = in[i];
+        out[i] = make_double2((double)v.x, (double)v.y);
+    }
+}
+
 // ------------------------------------------------------------------ launchers
-template <int LOGN>
+template <int LOGN, bool POINTS>
 static hipError_t tx_launch_n(const TxArgs& a, hipStream_t st)
 {
     using FS = FftShape<LOGN>;
     const size_t shm = sizeof(double2) * (FS::PADN + TwLds<LOGN>::SIZE + 256) + FS::N;  // + table + payload
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)tx_kernel<LOGN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+        (void)hipFuncSetAttribute((const void*)tx_kernel<LOGN, POINTS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)shm);
         attr = true;
     }
     const long nsym = a.nframes * a.S;
     if (nsym <= 0) return hipSuccess;
     // persistent grid: enough workgroups to fill every CU several times over
     const long grid = nsym < TX_MAX_GRID ? nsym : TX_MAX_GRID;
-    hipLaunchKernelGGL(tx_kernel<LOGN>, dim3((unsigned)grid), dim3(FS::T), shm, st, a);
+    hipLaunchKernelGGL((tx_kernel<LOGN, POINTS>), dim3((unsigned)grid), dim3(FS::T), shm, st, a);
     return hipGetLastError();
+}
+
+template <bool POINTS>
+static hipError_t launch_tx_p(int logn, const TxArgs& a, hipStream_t st)
+{
+    switch (logn) {
+        case 6: return tx_launch_n<6, POINTS>(a, st);
+        case 7: return tx_launch_n<7, POINTS>(a, st);
+        case 8: return tx_launch_n<8, POINTS>(a, st);
+        case 9: return tx_launch_n<9, POINTS>(a, st);
+        case 10: return tx_launch_n<10, POINTS>(a, st);
+        case 11: return tx_launch_n<11, POINTS>(a, st);
+        case 12: return tx_launch_n<12, POINTS>(a, st);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_tx(int logn, const TxArgs& a, hipStream_t st)
 {
-    switch (logn) {
-        case 6: return tx_launch_n<6>(a, st);
-        case 7: return tx_launch_n<7>(a, st);
-        case 8: return tx_launch_n<8>(a, st);
-        case 9: return tx_launch_n<9>(a, st);
-        case 10: return tx_launch_n<10>(a, st);
-        case 11: return tx_launch_n<11>(a, st);
-        case 12: return tx_launch_n<12>(a, st);
-        default: return hipErrorInvalidValue;
-    }
+    return a.points ? launch_tx_p<true>(logn, a, st) : launch_tx_p<false>(logn, a, st);
 }
 
 template <int LOGN>
@@ -551,6 +594,25 @@ hipError_t launch_map(const uint8_t* bytes, long nbytes, int k, const double2* t
     const int bs = 256;
     hipLaunchKernelGGL(map_kernel, dim3((unsigned)((npts + bs - 1) / bs)), dim3(bs), 0, st, bytes, nbytes, k, table,
                        out, npts);
+    return hipGetLastError();
+}
+
+hipError_t launch_bit_convert(const uint8_t* in, long len, int ib, int ob, uint8_t* out, long out_len, hipStream_t st)
+{
+    if (out_len <= 0) return hipSuccess;
+    const int bs = 256;
+    hipLaunchKernelGGL(bit_convert_kernel, dim3((unsigned)((out_len + bs - 1) / bs)), dim3(bs), 0, st, in, len, ib, ob,
+                       out, out_len);
+    return hipGetLastError();
+}
+
+hipError_t launch_i16_to_f64(const int16_t* in, long n, double* out, hipStream_t st)
+{
+    if (n <= 0) return hipSuccess;
+    long grid = (n + 255) / 256;
+    if (grid > 8192) grid = 8192;
+    hipLaunchKernelGGL(i16_to_f64_kernel, dim3((unsigned)grid), dim3(256), 0, st, reinterpret_cast<const short2*>(in), n,
+                       reinterpret_cast<double2*>(out));
     return hipGetLastError();
 }
 

@@ -84,6 +84,10 @@ SIGNATURES = {
     "ofdm_rx_demod": (_I, [_V, _V, _SZ, _SZ, _V, _SZ, _V, _V, _V, _V, _V]),
     "ofdm_demap": (_I, [_V, _V, _SZ, _V, _V]),
     "ofdm_map": (_I, [_V, _V, _SZ, _V, _V]),
+    "ofdm_fft_write": (_I, [_V, _V, _SZ, _V, _V]),
+    "ofdm_fft_read": (_I, [_V, _V, _SZ, _V, _V]),
+    "ofdm_bit_convert": (_I, [_V, _V, _SZ, _I, _I, _V, C.POINTER(_SZ), _V]),
+    "ofdm_int16_to_double": (_I, [_V, _V, _SZ, _V, _V]),
     "ofdm_t2_scan": (_I, [_V, _V, _SZ, _L, _V, _V, _V]),
     "ofdm_find_preamble": (_I, [_V, _V, _SZ, _V, _SZ, _V, _V]),
     "ofdm_cfo_estimate": (_I, [_V, _V, _SZ, _SZ, _I, _V, _V]),
@@ -223,6 +227,21 @@ class Modem:
 
     def map(self, data, nbytes: int, points_out, stream=None):
         check(lib().ofdm_map(self.h, _ptr(data), nbytes, _ptr(points_out), _stream(stream)))
+
+    def fft_write(self, points, nframes: int, fft_buf, stream=None):
+        check(lib().ofdm_fft_write(self.h, _ptr(points), nframes, _ptr(fft_buf), _stream(stream)))
+
+    def fft_read(self, fft_buf, nframes: int, restored, stream=None):
+        check(lib().ofdm_fft_read(self.h, _ptr(fft_buf), nframes, _ptr(restored), _stream(stream)))
+
+    def bit_convert(self, data, n: int, in_bits: int, out_bits: int, out, stream=None) -> int:
+        m = C.c_size_t()
+        check(lib().ofdm_bit_convert(self.h, _ptr(data), n, in_bits, out_bits, _ptr(out), C.byref(m),
+                                     _stream(stream)))
+        return m.value
+
+    def int16_to_double(self, iq16, n: int, out, stream=None):
+        check(lib().ofdm_int16_to_double(self.h, _ptr(iq16), n, _ptr(out), _stream(stream)))
 
     def t2_scan(self, iq, n: int, start: int, rel_out=None, first_out=None, stream=None):
         check(lib().ofdm_t2_scan(self.h, _ptr(iq), n, start, _ptr(rel_out), _ptr(first_out),

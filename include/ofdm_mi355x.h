@@ -175,6 +175,25 @@ int ofdm_demap(ofdm_ctx* ctx, double* points, size_t n, uint8_t* bytes_out, void
 /* Modulation::mod alone (modulation.cpp:39-50): nbytes -> nbytes*8/k points. */
 int ofdm_map(ofdm_ctx* ctx, const uint8_t* bytes, size_t nbytes, double* points_out, void* stream);
 
+/* FFT_FORM::write (Frame.cpp:54-70) on given points: per frame, D*num_symb
+ * constellation points -> FFT_buf layout (num_symb bodies of N samples, no
+ * CP): zero, pilots, segments, unnormalised IFFT, /sqrt(N). Device buffers. */
+int ofdm_fft_write(ofdm_ctx* ctx, const double* points, size_t nframes, double* fft_buf, void* stream);
+/* FFT_FORM::read (Frame.cpp:73-96) on an FFT_buf layout (num_symb bodies of
+ * N samples per frame, no CP) -> restored D*num_symb points per frame. The
+ * input is not modified (the reference transforms FFT_buf in place). */
+int ofdm_fft_read(ofdm_ctx* ctx, const double* fft_buf, size_t nframes, double* restored, void* stream);
+
+/* Modulation::bit_stream_converter (modulation.cpp:90-125): MSB-first repack
+ * of len in_bits-wide units into ceil(len*in_bits/out_bits) out_bits-wide
+ * units, last one left-aligned; *out_len receives the count. 1 <= bits <= 8. */
+int ofdm_bit_convert(ofdm_ctx* ctx, const uint8_t* in, size_t len, int in_bits, int out_bits,
+                     uint8_t* out, size_t* out_len, void* stream);
+
+/* FRAME_FORM::form_int16_to_double (Frame.hpp:472-481): n complex<int16>
+ * samples -> n complex<double>. Device buffers. */
+int ofdm_int16_to_double(ofdm_ctx* ctx, const int16_t* in, size_t n, double* out, void* stream);
+
 /* ---- rx sync front end ----------------------------- */
 /* T2SIN_FORM::corr (Frame.hpp:96-147) over all floor((n-start)/t2sin_size)
  * blocks from `start`: rel_out[b] = energy ratio if > level else 0 (device,

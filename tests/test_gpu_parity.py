@@ -240,3 +240,51 @@ def test_invalid_arguments_raise():
         M.Modem(dict(ALL_CONFIGS["D"], fft_size=500))
     with pytest.raises(M.OfdmError):
         M.Modem(dict(ALL_CONFIGS["D"], mod_type=3))
+
+
+@pytest.mark.parametrize("name", ["D", "B", "N64_k1", "D_s12_staged"])
+def test_fft_form_write_read_match_oracle(name):
+    """FFT_FORM::write / ::read (Frame.cpp:54-96) on FFT_buf layouts."""
+    cfg = ALL_CONFIGS[name]
+    m = modem(name)
+    N, D, P, S = cfg["fft_size"], cfg["num_data_subc"], cfg["num_pilot_subc"], cfg["num_symb"]
+    ampl = cfg["pilot_ampl"] / 1000
+    nf = 3
+    rng = np.random.default_rng(4)
+    pts = O.constellation(cfg["mod_type"])[rng.integers(0, 1 << cfg["mod_type"], nf * D * S)]
+    fb = torch.zeros((nf * N * S,), dtype=torch.complex128, device="cuda")
+    m.fft_write(dev(pts), nf, fb)
+    ref_fb = np.concatenate([(lambda o: (O.lib().orc_fft_write(N, D, P, S, ampl, O._d(pts[f * D * S:(f + 1) * D * S].copy()), O._d(o)), o)[1])(np.zeros(N * S, np.complex128)) for f in range(nf)])
+    assert rel_err(host(fb), ref_fb) < TOL
+    noisy = O.awgn(ref_fb, 0.05, seed=3)
+    rest = torch.zeros((nf * D * S,), dtype=torch.complex128, device="cuda")
+    m.fft_read(dev(noisy), nf, rest)
+    want = []
+    for f in range(nf):
+        buf = noisy[f * N * S:(f + 1) * N * S].copy()
+        o = np.zeros(D * S, np.complex128)
+        O.lib().orc_fft_read(N, D, P, S, ampl, O._d(buf), O._d(o))
+        want.append(o)
+    assert rel_err(host(rest), np.concatenate(want)) < TOL
+
+
+@pytest.mark.parametrize("ib,ob", [(8, 1), (8, 2), (8, 4), (8, 6), (8, 8), (1, 8), (2, 8), (4, 8), (6, 8), (3, 5)])
+def test_bit_convert_matches_oracle(ib, ob):
+    m = modem("D")
+    rng = np.random.default_rng(ib * 10 + ob)
+    for n in (1, 7, 1000):
+        data = rng.integers(0, 1 << ib, n, dtype=np.uint8)
+        out = torch.zeros((n * 8 + 8,), dtype=torch.uint8, device="cuda")
+        k = m.bit_convert(dev(data), n, ib, ob, out)
+        want = O.bit_convert(ob, ib, data)
+        assert k == len(want)
+        assert np.array_equal(host(out)[:k], want)
+
+
+def test_int16_to_double():
+    m = modem("D")
+    v = np.random.default_rng(0).integers(-32768, 32767, 2 * 10007, dtype=np.int16)
+    out = torch.zeros((10007,), dtype=torch.complex128, device="cuda")
+    m.int16_to_double(dev(v), 10007, out)
+    h = host(out)
+    assert np.array_equal(h.real, v[0::2].astype(np.float64)) and np.array_equal(h.imag, v[1::2].astype(np.float64))
