@@ -1,0 +1,418 @@
+// Frame.cpp — the FFT_FORM / T2SIN_FORM / OFDM_FORM / PREAMBLE_FORM /
+// FRAME_FORM members of the compatibility layer. Each DSP member stages its
+// host buffers to the device, runs the C-ABI entry (HIP kernels) and copies
+// the result back with the reference's in-place semantics.
+#include "OFDM/Frame.hpp"
+
+#include <cstdio>
+#include <cstdlib>
+
+#include "ofdm_compat.hpp"
+
+using ofdm_compat::check;
+using ofdm_compat::Context;
+
+namespace {
+
+constexpr size_t CD = sizeof(complex_double);
+
+// OFDM_COMPAT_TRACE=1: one stderr line per compat call (diagnostics).
+bool trace_on()
+{
+    static const bool on = std::getenv("OFDM_COMPAT_TRACE") != nullptr;
+    return on;
+}
+#define COMPAT_TRACE(name)                                           \
+    do {                                                             \
+        if (trace_on()) std::fprintf(stderr, "[compat] %s\n", name); \
+    } while (0)
+
+ofdm_params form_params(ConfigMap& config, int num_symb, int mod)
+{
+    ofdm_params p = ofdm_compat::params_from(config);
+    p.num_symb = num_symb;
+    p.mod_type = mod;
+    return p;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- FFT_FORM
+FFT_FORM::FFT_FORM(int fft_size, int num_data_subc, int num_pilot_subc, int num_symb, double pilot_ampl)
+    : fft_size(fft_size),
+      num_data_subc(num_data_subc),
+      num_pilot_subc(num_pilot_subc),
+      num_symb(num_symb),
+      segment_step(num_data_subc / num_pilot_subc + 1),
+      segment_size(segment_step - 1),
+      segment_byte_size(segment_size * (int)sizeof(complex_double)),
+      FFT_buf((size_t)num_symb * fft_size, complex_double(0.0, 0.0)),
+      segment((size_t)num_pilot_subc * num_symb, nullptr),
+      pilot((size_t)num_pilot_subc * num_symb, nullptr),
+      restored_buf((size_t)num_data_subc * num_symb, 0),
+      norm_factor(std::sqrt(static_cast<double>(fft_size))),
+      pilot_ampl(pilot_ampl)
+{
+    COMPAT_TRACE("FFT_FORM::FFT_FORM");
+    // pilot comb / segment pointers into FFT_buf (the layout of Frame.cpp:31-44)
+    const int half = num_pilot_subc / 2;
+    for (int s = 0; s < num_symb; ++s) {
+        complex_double* base = FFT_buf.data() + (size_t)s * fft_size;
+        int j = 0;
+        for (int pos = 1 + segment_size; j < half; ++j, pos += segment_step) {
+            pilot[s * num_pilot_subc + j] = base + pos;
+            segment[s * num_pilot_subc + j] = base + pos - segment_size;
+        }
+        for (int pos = fft_size - segment_step * half; j < num_pilot_subc; ++j, pos += segment_step) {
+            pilot[s * num_pilot_subc + j] = base + pos;
+            segment[s * num_pilot_subc + j] = base + pos + 1;
+        }
+    }
+    ofdm_params p = ofdm_compat::params_default();
+    p.fft_size = fft_size;
+    p.num_data_subc = num_data_subc;
+    p.num_pilot_subc = num_pilot_subc;
+    p.num_symb = num_symb;
+    p.cp_size = 0;
+    p.mod_type = 8;  // unused by FFT_FORM; any k keeps D*S*k byte-aligned
+    p.pilot_ampl = std::lround(pilot_ampl * 1000);
+    p.pr_sin_len = std::min<long>(p.pr_sin_len, fft_size);
+    ctx_ = ofdm_compat::context_for(p);
+}
+
+FFT_FORM::~FFT_FORM() = default;
+
+void FFT_FORM::write(complex_vector& input)
+{
+    COMPAT_TRACE("FFT_FORM::write");
+    const size_t np = (size_t)num_data_subc * num_symb;
+    complex_vector pts(np, 0);
+    std::copy_n(input.begin(), std::min(np, input.size()), pts.begin());
+    void* din = ctx_->buf(0, np * CD);
+    void* dout = ctx_->buf(1, FFT_buf.size() * CD);
+    ctx_->h2d(din, pts.data(), np * CD);
+    check(ofdm_fft_write(ctx_->ctx, (const double*)din, 1, (double*)dout, nullptr), "ofdm_fft_write");
+    ctx_->d2h(FFT_buf.data(), dout, FFT_buf.size() * CD);
+}
+
+complex_vector& FFT_FORM::read()
+{
+    COMPAT_TRACE("FFT_FORM::read");
+    void* din = ctx_->buf(0, FFT_buf.size() * CD);
+    void* dout = ctx_->buf(1, restored_buf.size() * CD);
+    ctx_->h2d(din, FFT_buf.data(), FFT_buf.size() * CD);
+    check(ofdm_fft_read(ctx_->ctx, (const double*)din, 1, (double*)dout, nullptr), "ofdm_fft_read");
+    ctx_->d2h(restored_buf.data(), dout, restored_buf.size() * CD);
+    return restored_buf;
+}
+
+// ---------------------------------------------------------------- T2SIN_FORM
+T2SIN_FORM::T2SIN_FORM(ConfigMap& config)
+    : config(config),
+      size((int)config["T2sin_size"]),
+      f1((int)config["T2_sin_f1"]),
+      f2((int)config["T2_sin_f2"]),
+      smooth((int)config["smooth"]),
+      level((double)config["T2_sin_level"] / 1000),
+      detect_mask(size, 0.0),
+      detect_buf(size, complex_double(0, 0)),
+      mean_freq((f1 + f2) / 2),
+      min_f1(std::max(0, f1 - smooth)),
+      max_f1(std::max(mean_freq, f1 + smooth)),
+      min_f2(std::max(mean_freq, f2 - smooth)),
+      max_f2(std::max(size, f2 + smooth))
+{
+    COMPAT_TRACE("T2SIN_FORM::T2SIN_FORM");
+    // detector mask (Frame.cpp:120-133): +1 on [f-smooth, f+smooth] clamped, per tone
+    for (int f : {f1, f2})
+        for (int i = std::max(0, f - smooth); i <= std::min(size - 1, f + smooth); ++i) detect_mask[i] += 1.0;
+    ctx_ = ofdm_compat::context_for(ofdm_compat::params_from(config));
+}
+
+void T2SIN_FORM::set(complex_double* buf_ptr)
+{
+    COMPAT_TRACE("T2SIN_FORM::set");
+    buf = buf_ptr;
+    if (size) check(ofdm_get_t2_symbol(ctx_->ctx, reinterpret_cast<double*>(buf)), "ofdm_get_t2_symbol");
+}
+
+std::vector<double> T2SIN_FORM::corr(complex_vector& signal)
+{
+    COMPAT_TRACE("T2SIN_FORM::corr");
+    const size_t n = signal.size();
+    std::vector<double> out(size ? n / size : 0, 0.0);
+    if (out.empty()) return out;
+    void* dx = ctx_->buf(0, n * CD);
+    void* dr = ctx_->buf(1, out.size() * sizeof(double));
+    ctx_->h2d(dx, signal.data(), n * CD);
+    check(ofdm_t2_scan(ctx_->ctx, (const double*)dx, n, 0, (double*)dr, nullptr, nullptr), "ofdm_t2_scan");
+    ctx_->d2h(out.data(), dr, out.size() * sizeof(double));
+    return out;
+}
+
+int T2SIN_FORM::find_t2sin(complex_vector& signal, int start_index)
+{
+    COMPAT_TRACE("T2SIN_FORM::find_t2sin");
+    const size_t n = signal.size();
+    void* dx = ctx_->buf(0, n * CD);
+    int* df = (int*)ctx_->buf(2, sizeof(int));
+    ctx_->h2d(dx, signal.data(), n * CD);
+    check(ofdm_t2_scan(ctx_->ctx, (const double*)dx, n, start_index, nullptr, df, nullptr), "ofdm_t2_scan");
+    int first = -1;
+    ctx_->d2h(&first, df, sizeof(int));
+    return first;
+}
+
+// ---------------------------------------------------------------- OFDM_FORM
+OFDM_FORM::OFDM_FORM(ConfigMap& config, bool data, bool with_preamble)
+    : config(config),
+      data(data),
+      fft_size((int)config["fft_size"]),
+      num_data_subc((int)config["num_data_subc"]),
+      num_pilot_subc((int)config["num_pilot_subc"]),
+      cp_size((int)config["cp_size"]),
+      num_symb((int)((with_preamble) ? config["num_symb"] + config["num_pr_symb"]
+                                     : (data) ? config["num_symb"] : config["num_pr_symb"])),
+      pr_sin_len((int)config["pr_sin_len"]),
+      pr_seed((int)config["pr_seed"]),
+      modType((data) ? static_cast<mod_type>(config["modType"]) : mod_type(1)),
+      ofdm_len(fft_size + cp_size),
+      size((fft_size + cp_size) * num_symb),
+      usefull_size(num_data_subc * num_symb),
+      output(num_symb, nullptr),
+      fft_task(fft_size, num_data_subc, num_pilot_subc, num_symb, double(config["pilot_ampl"]) / 1000),
+      Mod(modType),
+      byte_fft_size(fft_size * (int)sizeof(complex_double)),
+      pilot_ampl((int)config["pilot_ampl"])
+{
+    COMPAT_TRACE("OFDM_FORM::OFDM_FORM");
+    ctx_ = ofdm_compat::context_for(form_params(config, num_symb, modType));
+}
+
+void OFDM_FORM::set(complex_double* buf_ptr)
+{
+    COMPAT_TRACE("OFDM_FORM::set");
+    for (int i = 0; i < num_symb; i++) output[i] = buf_ptr + (size_t)(cp_size + fft_size) * i;
+}
+
+void OFDM_FORM::write(bit_vector& input)
+{
+    COMPAT_TRACE("OFDM_FORM::write");
+    const size_t nb = (size_t)ctx_->geo.bytes_per_frame;
+    bit_vector bytes(nb, 0);
+    std::copy_n(input.begin(), std::min(nb, input.size()), bytes.begin());
+    void* db = ctx_->buf(0, nb);
+    void* dx = ctx_->buf(1, (size_t)size * CD);
+    ctx_->h2d(db, bytes.data(), nb);
+    check(ofdm_tx_modulate(ctx_->ctx, (const uint8_t*)db, 1, (double*)dx, (size_t)size, nullptr, nullptr, nullptr),
+          "ofdm_tx_modulate");
+    ctx_->d2h(output[0], dx, (size_t)size * CD);
+}
+
+bit_vector OFDM_FORM::read()
+{
+    COMPAT_TRACE("OFDM_FORM::read");
+    const size_t nb = ((size_t)usefull_size * modType + 7) / 8;
+    bit_vector out(nb);
+    void* dx = ctx_->buf(1, (size_t)size * CD);
+    void* db = ctx_->buf(0, nb);
+    ctx_->h2d(dx, output[0], (size_t)size * CD);
+    check(ofdm_rx_demod(ctx_->ctx, (const double*)dx, 1, (size_t)size, nullptr, 0, nullptr, (uint8_t*)db, nullptr,
+                        nullptr, nullptr),
+          "ofdm_rx_demod");
+    ctx_->d2h(out.data(), db, nb);
+    return out;
+}
+
+complex_vector OFDM_FORM::fft()
+{
+    COMPAT_TRACE("OFDM_FORM::fft");
+    const size_t np = (size_t)usefull_size;
+    void* dx = ctx_->buf(1, (size_t)size * CD);
+    void* dc = ctx_->buf(2, np * CD);
+    ctx_->h2d(dx, output[0], (size_t)size * CD);
+    check(ofdm_rx_demod(ctx_->ctx, (const double*)dx, 1, (size_t)size, nullptr, 0, (double*)dc, nullptr, nullptr,
+                        nullptr, nullptr),
+          "ofdm_rx_demod");
+    ctx_->d2h(fft_task.restored_buf.data(), dc, np * CD);
+    return fft_task.restored_buf;
+}
+
+void OFDM_FORM::cp_freq_sinh()
+{
+    COMPAT_TRACE("OFDM_FORM::cp_freq_sinh");
+    void* dx = ctx_->buf(1, (size_t)size * CD);
+    ctx_->h2d(dx, output[0], (size_t)size * CD);
+    check(ofdm_cp_sync(ctx_->ctx, (double*)dx, 1, (size_t)size, num_symb, nullptr), "ofdm_cp_sync");
+    ctx_->d2h(output[0], dx, (size_t)size * CD);
+}
+
+void OFDM_FORM::pr_phase_sinh(complex_double* pr, int pr_size)
+{
+    COMPAT_TRACE("OFDM_FORM::pr_phase_sinh");
+    void* dx = ctx_->buf(1, (size_t)size * CD);
+    void* dp = ctx_->buf(3, (size_t)pr_size * CD);
+    ctx_->h2d(dx, output[0], (size_t)size * CD);
+    ctx_->h2d(dp, pr, (size_t)pr_size * CD);
+    check(ofdm_phase_sync(ctx_->ctx, (double*)dx, 1, (size_t)size, (size_t)size, (const double*)dp, (size_t)pr_size,
+                          nullptr),
+          "ofdm_phase_sync");
+    ctx_->d2h(output[0], dx, (size_t)size * CD);
+}
+
+double OFDM_FORM::pilot_freq_sinh()
+{
+    COMPAT_TRACE("OFDM_FORM::pilot_freq_sinh");
+    void* dx = ctx_->buf(1, (size_t)size * CD);
+    void* dc = ctx_->buf(4, sizeof(double));
+    ctx_->h2d(dx, output[0], (size_t)size * CD);
+    check(ofdm_cfo_estimate(ctx_->ctx, (const double*)dx, 1, (size_t)size, num_symb, (double*)dc, nullptr),
+          "ofdm_cfo_estimate");
+    double shift = 0;
+    ctx_->d2h(&shift, dc, sizeof(double));
+    return shift;
+}
+
+void OFDM_FORM::freq_shift(double& shift)
+{
+    COMPAT_TRACE("OFDM_FORM::freq_shift");
+    void* dx = ctx_->buf(1, (size_t)size * CD);
+    void* dc = ctx_->buf(4, sizeof(double));
+    ctx_->h2d(dx, output[0], (size_t)size * CD);
+    ctx_->h2d(dc, &shift, sizeof(double));
+    check(ofdm_freq_shift(ctx_->ctx, (double*)dx, 1, (size_t)size, (size_t)size, (const double*)dc, nullptr),
+          "ofdm_freq_shift");
+    ctx_->d2h(output[0], dx, (size_t)size * CD);
+}
+
+// ---------------------------------------------------------------- PREAMBLE_FORM
+PREAMBLE_FORM::PREAMBLE_FORM(ConfigMap& config)
+    : OFDM_FORM(config, false),
+      level((double)config["pr_level"] / 1000),
+      preamble((size_t)usefull_size * modType / 8, 0),
+      mod_preamble(size, complex_double(0, 0)),
+      ofdm_preamble(size, complex_double(0, 0)),
+      conjected_sinh_part(pr_sin_len, complex_double(0, 0)),
+      cor((size_t)config["T2sin_size"] * 2 + pr_sin_len, 0.0),
+      chan_est(num_data_subc, complex_double(0, 0))
+{
+    COMPAT_TRACE("PREAMBLE_FORM::PREAMBLE_FORM");
+    // mt19937(pr_seed) bytes, made by the context exactly as Frame.cpp:269-272
+    check(ofdm_get_preamble(ctx_->ctx, preamble.data(), nullptr, nullptr, nullptr), "ofdm_get_preamble");
+}
+
+void PREAMBLE_FORM::set(complex_double* buf_ptr)
+{
+    COMPAT_TRACE("PREAMBLE_FORM::set");
+    OFDM_FORM::set(buf_ptr);
+    write(preamble);  // BPSK OFDM preamble on the GPU into the frame buffer
+    std::copy_n(output[0], ofdm_preamble.size(), ofdm_preamble.begin());
+    mod_preamble = Mod.mod(preamble);
+    check(ofdm_get_preamble(ctx_->ctx, nullptr, nullptr, nullptr, reinterpret_cast<double*>(conjected_sinh_part.data())),
+          "ofdm_get_preamble");
+}
+
+void PREAMBLE_FORM::find_corr(complex_vector& input, int start)
+{
+    COMPAT_TRACE("PREAMBLE_FORM::find_corr");
+    const size_t n = input.size();
+    void* dx = ctx_->buf(5, n * CD);
+    void* dc = ctx_->buf(6, cor.size() * sizeof(double));
+    ctx_->h2d(dx, input.data(), n * CD);
+    check(ofdm_preamble_corr(ctx_->ctx, (const double*)dx, n, start, (double*)dc, nullptr), "ofdm_preamble_corr");
+    ctx_->d2h(cor.data(), dc, cor.size() * sizeof(double));
+}
+
+int PREAMBLE_FORM::find_preamble(complex_vector& input, int start)
+{
+    COMPAT_TRACE("PREAMBLE_FORM::find_preamble");
+    const size_t n = input.size();
+    void* dx = ctx_->buf(5, n * CD);
+    int* ds = (int*)ctx_->buf(7, 2 * sizeof(int));
+    ctx_->h2d(dx, input.data(), n * CD);
+    ctx_->h2d(ds, &start, sizeof(int));
+    check(ofdm_find_preamble(ctx_->ctx, (const double*)dx, n, ds, 1, ds + 1, nullptr), "ofdm_find_preamble");
+    int idx = -10;
+    ctx_->d2h(&idx, ds + 1, sizeof(int));
+    return idx;
+}
+
+complex_vector PREAMBLE_FORM::chan_char()
+{
+    COMPAT_TRACE("PREAMBLE_FORM::chan_char");
+    // the unused averaging estimator (Frame.hpp:375-385) on the GPU FFT output
+    complex_vector pr = fft();
+    std::fill(chan_est.begin(), chan_est.end(), complex_double(0.0, 0.0));
+    for (int i = 0; i < num_data_subc * num_symb; i++) chan_est[i % num_data_subc] += pr[i] / mod_preamble[i];
+    for (int i = 0; i < num_data_subc; i++) chan_est[i] /= complex_double(num_symb, 0);
+    return chan_est;
+}
+
+complex_vector& PREAMBLE_FORM::chan_char_lq()
+{
+    COMPAT_TRACE("PREAMBLE_FORM::chan_char_lq");
+    void* dx = ctx_->buf(1, (size_t)size * CD);
+    void* dc = ctx_->buf(2, chan_est.size() * CD);
+    ctx_->h2d(dx, output[0], (size_t)size * CD);
+    check(ofdm_chan_estimate(ctx_->ctx, (const double*)dx, 1, (size_t)size, (double*)dc, chan_est.size(), nullptr),
+          "ofdm_chan_estimate");
+    ctx_->d2h(chan_est.data(), dc, chan_est.size() * CD);
+    return chan_est;
+}
+
+// ---------------------------------------------------------------- FRAME_FORM
+FRAME_FORM::FRAME_FORM(const std::string& CONFIGNAME)
+    : config(parse_config(CONFIGNAME)),
+      t2sin(config),
+      preamble(config),
+      message(config),
+      message_with_preamble(config, true, true),
+      buf(t2sin.size + preamble.size + message.size, complex_double(0.0, 0.0)),
+      int16_buf(buf.size()),
+      from_sdr_buf(buf.size() * (config["rx_buf_size"] + 1), complex_double(0.0, 0.0)),
+      from_sdr_int16_buf(from_sdr_buf.size()),
+      usefull_size(message.usefull_size * message.modType / 8),
+      output_size((int)buf.size()),
+      bit_preambple(usefull_size, 0)
+{
+    COMPAT_TRACE("FRAME_FORM::FRAME_FORM");
+    t2sin.set(buf.data());
+    preamble.set(buf.data() + t2sin.size);
+    message.set(buf.data() + t2sin.size + preamble.size);
+    message_with_preamble.set(buf.data() + t2sin.size);
+}
+
+void FRAME_FORM::write(bit_vector& input) { message.write(input); }
+
+bit_vector FRAME_FORM::read(void* transmitted_data)
+{
+    COMPAT_TRACE("FRAME_FORM::read");
+    std::memcpy(buf.data(), transmitted_data, sizeof(complex_double) * buf.size());
+    return message.read();
+}
+
+complex_vector FRAME_FORM::get() { return buf; }
+
+complex16_vector FRAME_FORM::get_int16()
+{
+    COMPAT_TRACE("FRAME_FORM::get_int16");
+    auto& ctx = message.ctx_;
+    void* dx = ctx->buf(1, buf.size() * CD);
+    void* d16 = ctx->buf(3, buf.size() * sizeof(std::complex<int16_t>));
+    ctx->h2d(dx, buf.data(), buf.size() * CD);
+    check(ofdm_double_to_int16(ctx->ctx, (const double*)dx, buf.size(), (int16_t*)d16, nullptr), "ofdm_double_to_int16");
+    ctx->d2h(int16_buf.data(), d16, buf.size() * sizeof(std::complex<int16_t>));
+    return int16_buf;
+}
+
+void FRAME_FORM::form_int16_to_double()
+{
+    COMPAT_TRACE("FRAME_FORM::form_int16_to_double");
+    auto& ctx = message.ctx_;
+    const size_t n = from_sdr_int16_buf.size();
+    void* d16 = ctx->buf(6, n * sizeof(std::complex<int16_t>));
+    void* dx = ctx->buf(5, n * CD);
+    ctx->h2d(d16, from_sdr_int16_buf.data(), n * sizeof(std::complex<int16_t>));
+    check(ofdm_int16_to_double(ctx->ctx, (const int16_t*)d16, n, (double*)dx, nullptr), "ofdm_int16_to_double");
+    ctx->d2h(from_sdr_buf.data(), dx, n * CD);
+}

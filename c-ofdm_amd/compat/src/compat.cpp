@@ -1,0 +1,231 @@
+// compat.cpp — plumbing (cached contexts, staging), parse_config, psk/qam and
+// Modulation of the C++ compatibility layer. Every DSP call goes through the
+// C-ABI of include/ofdm_mi355x.h (HIP kernels); there is no CPU DSP path.
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
+#include <cctype>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <stdexcept>
+
+#include "OFDM/modulation.hpp"
+#include "ofdm_compat.hpp"
+
+// ---------------------------------------------------------------- parser
+ConfigMap parse_config(const std::string& filename)
+{
+    std::ifstream file(filename);
+    if (!file.is_open()) throw std::runtime_error("Cannot open config file");
+    ConfigMap cfg;
+    std::string line;
+    auto not_space = [](unsigned char ch) { return !std::isspace(ch); };
+    while (std::getline(file, line)) {
+        line.erase(line.begin(), std::find_if(line.begin(), line.end(), not_space));
+        line.erase(std::find_if(line.rbegin(), line.rend(), not_space).base(), line.end());
+        if (line.empty() || line[0] == '#') continue;
+        const auto pos = line.find('=');
+        if (pos == std::string::npos) continue;
+        std::string key = line.substr(0, pos), value = line.substr(pos + 1);
+        key.erase(std::remove_if(key.begin(), key.end(), ::isspace), key.end());
+        value.erase(std::remove_if(value.begin(), value.end(), ::isspace), value.end());
+        cfg[key] = std::stol(value);
+    }
+    return cfg;
+}
+
+namespace ofdm_compat {
+
+// OFDM_COMPAT_TRACE set: print a raw backtrace on SIGSEGV/SIGABRT (diagnostics
+// for apps linked against the drop-in layer; symbolise with addr2line).
+static void crash_handler(int sig)
+{
+    void* frames[64];
+    const int n = backtrace(frames, 64);
+    const char msg[] = "[compat] fatal signal, backtrace:\n";
+    ssize_t w = write(2, msg, sizeof msg - 1);
+    (void)w;
+    backtrace_symbols_fd(frames, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+
+static struct CrashHandlerInstaller {
+    CrashHandlerInstaller()
+    {
+        if (std::getenv("OFDM_COMPAT_TRACE")) {
+            signal(SIGSEGV, crash_handler);
+            signal(SIGABRT, crash_handler);
+        }
+    }
+} g_crash_handler_installer;
+
+void check(int rc, const char* what)
+{
+    if (rc != OFDM_OK) throw std::runtime_error(std::string(what) + ": " + ofdm_last_error());
+}
+
+static int device_index()
+{
+    const char* e = std::getenv("OFDM_DEVICE");
+    return e ? std::atoi(e) : 0;
+}
+
+Context::Context(const ofdm_params& p) : params(p)
+{
+    check(ofdm_create(&params, device_index(), &ctx), "ofdm_create");
+    check(ofdm_get_geometry(ctx, &geo), "ofdm_get_geometry");
+}
+
+Context::~Context()
+{
+    for (auto& s : slots_)
+        if (s.first) ofdm_device_free(ctx, s.first);
+    ofdm_destroy(ctx);
+}
+
+void* Context::buf(int slot, size_t bytes)
+{
+    if ((int)slots_.size() <= slot) slots_.resize(slot + 1, {nullptr, 0});
+    auto& s = slots_[slot];
+    if (s.second < bytes) {
+        if (s.first) ofdm_device_free(ctx, s.first);
+        s.first = nullptr;
+        check(ofdm_device_alloc(ctx, bytes, &s.first), "ofdm_device_alloc");
+        s.second = bytes;
+    }
+    return s.first;
+}
+
+void Context::h2d(void* dev, const void* host, size_t bytes)
+{
+    if (bytes) check(ofdm_memcpy_h2d(ctx, dev, host, bytes, nullptr), "ofdm_memcpy_h2d");
+}
+
+void Context::d2h(void* host, const void* dev, size_t bytes)
+{
+    if (bytes) check(ofdm_memcpy_d2h(ctx, host, dev, bytes, nullptr), "ofdm_memcpy_d2h");
+    sync();
+}
+
+void Context::sync() { check(ofdm_stream_synchronize(ctx, nullptr), "ofdm_stream_synchronize"); }
+
+std::shared_ptr<Context> context_for(const ofdm_params& p)
+{
+    static std::mutex mu;
+    static std::map<std::string, std::weak_ptr<Context>> cache;
+    const std::string key(reinterpret_cast<const char*>(&p), sizeof p);
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find(key);
+    if (it != cache.end())
+        if (auto sp = it->second.lock()) return sp;
+    auto sp = std::make_shared<Context>(p);
+    cache[key] = sp;
+    return sp;
+}
+
+ofdm_params params_default()
+{
+    ofdm_params p;
+    check(ofdm_params_default(&p), "ofdm_params_default");
+    return p;
+}
+
+ofdm_params params_from(ConfigMap& c)
+{
+    ofdm_params p{};
+    p.fft_size = c["fft_size"];
+    p.num_data_subc = c["num_data_subc"];
+    p.num_pilot_subc = c["num_pilot_subc"];
+    p.cp_size = c["cp_size"];
+    p.num_symb = c["num_symb"];
+    p.num_pr_symb = c["num_pr_symb"];
+    p.pr_sin_len = c["pr_sin_len"];
+    p.pr_seed = c["pr_seed"];
+    p.pr_level = c["pr_level"];
+    p.t2sin_size = c["T2sin_size"];
+    p.t2_sin_f1 = c["T2_sin_f1"];
+    p.t2_sin_f2 = c["T2_sin_f2"];
+    p.t2_sin_level = c["T2_sin_level"];
+    p.smooth = c["smooth"];
+    p.mod_type = c["modType"];
+    p.pilot_ampl = c["pilot_ampl"];
+    p.mult = c["mult"];
+    p.rx_buf_size = c["rx_buf_size"];
+    p.iterations = c["iterations"];
+    return p;
+}
+
+}  // namespace ofdm_compat
+
+using ofdm_compat::check;
+
+// ---------------------------------------------------------------- Modulation
+// psk / qam: the constellation formulas of modulation.cpp:4-20 (table build, host).
+complex_double psk(uint8_t input, double angle, int deg)
+{
+    const double step = M_PI * 2 / (double)deg;
+    const complex_double j(0.0, 1.0);
+    return std::exp(j * (step * complex_double(input) + angle));
+}
+
+complex_double qam(uint8_t input, int deg)
+{
+    if ((deg % 2) || deg > 8) return complex_double(0.0, 0.0);
+    const uint8_t num = (uint8_t)(1u << (deg / 2));
+    return complex_double(2.0 / (num - 1) * double(input % num) - 1.0, 2.0 / (num - 1) * double(input >> (deg / 2)) - 1.0);
+}
+
+Modulation::Modulation(mod_type mod) : modulation(mod), constell(1u << mod, 0), mod_index(mod)
+{
+    for (size_t i = 0; i < constell.size(); i++)
+        constell[i] = modulation == bpsk ? psk(uint8_t(i), M_PI_4 * 5, 2) : qam(uint8_t(i), (int)mod_index);
+    ofdm_params p = ofdm_compat::params_default();
+    p.mod_type = mod;
+    ctx_ = ofdm_compat::context_for(p);
+}
+
+complex_vector Modulation::mod(std::vector<uint8_t>& in)
+{
+    const size_t n = (in.size() * 8) / mod_index + ((in.size() * 8) % mod_index > 0);
+    complex_vector out(n);
+    if (in.empty()) return out;
+    void* din = ctx_->buf(0, in.size());
+    void* dout = ctx_->buf(1, n * sizeof(complex_double));
+    ctx_->h2d(din, in.data(), in.size());
+    check(ofdm_map(ctx_->ctx, (const uint8_t*)din, in.size(), (double*)dout, nullptr), "ofdm_map");
+    ctx_->d2h(out.data(), dout, n * sizeof(complex_double));
+    return out;
+}
+
+std::vector<uint8_t> Modulation::demod(complex_vector& in)
+{
+    const size_t n = in.size(), nb = (n * mod_index + 7) / 8;
+    std::vector<uint8_t> out(nb);
+    if (!n) return out;
+    void* dp = ctx_->buf(0, n * sizeof(complex_double));
+    void* db = ctx_->buf(1, nb);
+    ctx_->h2d(dp, in.data(), n * sizeof(complex_double));
+    check(ofdm_demap(ctx_->ctx, (double*)dp, n, (uint8_t*)db, nullptr), "ofdm_demap");
+    ctx_->d2h(out.data(), db, nb);
+    ctx_->d2h(in.data(), dp, n * sizeof(complex_double));  // clamped in place (modulation.cpp:70-75)
+    return out;
+}
+
+std::vector<uint8_t> Modulation::bit_stream_converter(size_t ob, size_t ib, std::vector<uint8_t>& in)
+{
+    const size_t total = in.size() * ib, n = total / ob + (total % ob > 0);
+    std::vector<uint8_t> out(n);
+    if (in.empty()) return out;
+    void* din = ctx_->buf(0, in.size());
+    void* dout = ctx_->buf(1, n);
+    ctx_->h2d(din, in.data(), in.size());
+    size_t m = 0;
+    check(ofdm_bit_convert(ctx_->ctx, (const uint8_t*)din, in.size(), (int)ib, (int)ob, (uint8_t*)dout, &m, nullptr),
+          "ofdm_bit_convert");
+    ctx_->d2h(out.data(), dout, n);
+    return out;
+}

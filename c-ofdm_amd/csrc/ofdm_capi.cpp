@@ -485,9 +485,13 @@ int ofdm_create(const ofdm_params* params, int device, ofdm_ctx** out)
         }
     }
     // T2 detector tables
+    if ((rc = upload(&c->d_first, std::vector<int>(4, 0)))) {
+        ofdm_destroy(c);
+        return rc;
+    }
     if (c->t2 >= 64 && c->t2 <= 4096 && ilog2_exact(c->t2) > 0) {
         c->t2_logn = ilog2_exact(c->t2);
-        if ((rc = upload(&c->d_t2tw, twiddles(c->t2))) || (rc = upload(&c->d_first, std::vector<int>(1, 0)))) {
+        if ((rc = upload(&c->d_t2tw, twiddles(c->t2)))) {
             ofdm_destroy(c);
             return rc;
         }
@@ -792,6 +796,15 @@ int ofdm_int16_to_double(ofdm_ctx* c, const int16_t* in, size_t n, double* out, 
     return OFDM_OK;
 }
 
+int ofdm_double_to_int16(ofdm_ctx* c, const double* in, size_t n, int16_t* out, void* stream)
+{
+    if (!c || (n && (!in || !out))) return fail(OFDM_ERR_INVALID, "null argument");
+    if (!aligned16(in) || ((uintptr_t)out & 3)) return fail(OFDM_ERR_INVALID, "misaligned buffers");
+    hipError_t e = ofdm::launch_f64_to_i16(in, (long)n, (double)c->p.mult, out, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "double_to_int16 launch");
+    return OFDM_OK;
+}
+
 // ---- sync front end (ofdm_sync.hip)
 int ofdm_t2_scan(ofdm_ctx* c, const double* iq, size_t n, long start, double* rel_out, int* first_out, void* stream)
 {
@@ -834,6 +847,31 @@ int ofdm_find_preamble(ofdm_ctx* c, const double* iq, size_t n, const int* start
     a.level = (double)c->p.pr_level / 1000;
     hipError_t e = ofdm::launch_find_preamble(a, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "find_preamble launch");
+    return OFDM_OK;
+}
+
+int ofdm_preamble_corr(ofdm_ctx* c, const double* iq, size_t n, long start, double* cor_out, void* stream)
+{
+    if (!c || !iq || !cor_out) return fail(OFDM_ERR_INVALID, "null argument");
+    if (!aligned16(iq)) return fail(OFDM_ERR_INVALID, "iq must be 16-byte aligned");
+    if (start < INT32_MIN || start > INT32_MAX) return fail(OFDM_ERR_INVALID, "start out of range");
+    int* d_start = c->d_first + 2;  // scratch word 2: the one start index
+    const int s32 = (int)start;
+    HIP_TRY(hipMemcpyAsync(d_start, &s32, sizeof(int), hipMemcpyHostToDevice, (hipStream_t)stream));
+    ofdm::PreambleArgs a{};
+    a.iq = reinterpret_cast<const double2*>(iq);
+    a.n = (long)n;
+    a.starts = d_start;
+    a.nstarts = 1;
+    a.idx_out = nullptr;
+    a.templ = c->d_templ;
+    a.L = (int)c->p.pr_sin_len;
+    a.cycles = (int)(2 * c->p.t2sin_size + c->p.pr_sin_len);
+    a.level = (double)c->p.pr_level / 1000;
+    a.cor_out = cor_out;
+    hipError_t e = ofdm::launch_find_preamble(a, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "preamble_corr launch");
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));  // the start word is host-staged
     return OFDM_OK;
 }
 

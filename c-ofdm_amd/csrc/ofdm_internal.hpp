@@ -64,6 +64,7 @@ hipError_t launch_map(const uint8_t* bytes, long nbytes, int k, const double2* t
 hipError_t launch_bit_convert(const uint8_t* in, long len, int in_bits, int out_bits, uint8_t* out, long out_len,
                               hipStream_t stream);
 hipError_t launch_i16_to_f64(const int16_t* in, long n, double* out, hipStream_t stream);
+hipError_t launch_f64_to_i16(const double* in, long n, double mult, int16_t* out, hipStream_t stream);
 
 // Register-resident rx limits: S*ceil(D/T) <= RX_REG_SLOTS.
 constexpr int RX_SMAX = 8;

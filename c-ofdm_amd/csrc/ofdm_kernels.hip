@@ -488,6 +488,15 @@ __global__ void i16_to_f64_kernel(const short2* __restrict__ in, long n, double2
     }
 }
 
+// FRAME_FORM::get_int16 on arbitrary samples: trunc(x * mult) per component.
+__global__ void f64_to_i16_kernel(const double2* __restrict__ in, long n, double mult, short2* __restrict__ out)
+{
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const double2 v = in[i];
+        out[i] = make_short2(to_int16(v.x * mult), to_int16(v.y * mult));
+    }
+}
+
 // ------------------------------------------------------------------ launchers
 template <int LOGN, bool POINTS>
 static hipError_t tx_launch_n(const TxArgs& a, hipStream_t st)
@@ -603,6 +612,16 @@ hipError_t launch_bit_convert(const uint8_t* in, long len, int ib, int ob, uint8
     const int bs = 256;
     hipLaunchKernelGGL(bit_convert_kernel, dim3((unsigned)((out_len + bs - 1) / bs)), dim3(bs), 0, st, in, len, ib, ob,
                        out, out_len);
+    return hipGetLastError();
+}
+
+hipError_t launch_f64_to_i16(const double* in, long n, double mult, int16_t* out, hipStream_t st)
+{
+    if (n <= 0) return hipSuccess;
+    long grid = (n + 255) / 256;
+    if (grid > 8192) grid = 8192;
+    hipLaunchKernelGGL(f64_to_i16_kernel, dim3((unsigned)grid), dim3(256), 0, st, reinterpret_cast<const double2*>(in),
+                       n, mult, reinterpret_cast<short2*>(out));
     return hipGetLastError();
 }
 

@@ -230,10 +230,13 @@ __global__ void __launch_bounds__(SYNC_THREADS) find_preamble_kernel(PreambleArg
         en[nl] = e;
     }
     __syncthreads();
+    double* cor = a.cor_out ? a.cor_out + (long)blockIdx.x * C : nullptr;
     nl = 0;
     for (int i = t; i < C && nl < 4; i += SYNC_THREADS, ++nl) {
         const double norm = normv[i];
-        if (norm > 1.0 && hypot(en[nl].x, en[nl].y) / sqrt(norm) > a.level) atomicMin(best, i);
+        const double r = norm > 1.0 ? hypot(en[nl].x, en[nl].y) / sqrt(norm) : 0.0;
+        if (cor) cor[i] = r;
+        if (norm > 1.0 && r > a.level) atomicMin(best, i);
     }
     // lags beyond 4*SYNC_THREADS (C > 1024): continue serially in chunks
     for (int base = 4 * SYNC_THREADS; base < C; base += SYNC_THREADS) {
@@ -242,11 +245,13 @@ __global__ void __launch_bounds__(SYNC_THREADS) find_preamble_kernel(PreambleArg
             double2 e = make_double2(0.0, 0.0);
             for (int j = 0; j < L; ++j) e = cadd_rn(e, cmul_exact(xs[i + j], c[j]));
             const double norm = normv[i];
-            if (norm > 1.0 && hypot(e.x, e.y) / sqrt(norm) > a.level) atomicMin(best, i);
+            const double r = norm > 1.0 ? hypot(e.x, e.y) / sqrt(norm) : 0.0;
+            if (cor) cor[i] = r;
+            if (norm > 1.0 && r > a.level) atomicMin(best, i);
         }
     }
     __syncthreads();
-    if (t == 0) a.idx_out[blockIdx.x] = *best == INT_MAX ? -10 : (int)(s + *best);
+    if (t == 0 && a.idx_out) a.idx_out[blockIdx.x] = *best == INT_MAX ? -10 : (int)(s + *best);
 }
 
 hipError_t launch_find_preamble(const PreambleArgs& a, hipStream_t st)

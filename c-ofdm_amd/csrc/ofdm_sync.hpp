@@ -28,6 +28,7 @@ struct PreambleArgs {
     int L;                  // pr_sin_len
     int cycles;             // 2*T2sin_size + pr_sin_len
     double level;           // pr_level / 1000
+    double* cor_out;        // nullable: find_corr values, cycles per start
 };
 
 struct CfoArgs {

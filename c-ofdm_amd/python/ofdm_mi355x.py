@@ -88,6 +88,8 @@ SIGNATURES = {
     "ofdm_fft_read": (_I, [_V, _V, _SZ, _V, _V]),
     "ofdm_bit_convert": (_I, [_V, _V, _SZ, _I, _I, _V, C.POINTER(_SZ), _V]),
     "ofdm_int16_to_double": (_I, [_V, _V, _SZ, _V, _V]),
+    "ofdm_double_to_int16": (_I, [_V, _V, _SZ, _V, _V]),
+    "ofdm_preamble_corr": (_I, [_V, _V, _SZ, _L, _V, _V]),
     "ofdm_t2_scan": (_I, [_V, _V, _SZ, _L, _V, _V, _V]),
     "ofdm_find_preamble": (_I, [_V, _V, _SZ, _V, _SZ, _V, _V]),
     "ofdm_cfo_estimate": (_I, [_V, _V, _SZ, _SZ, _I, _V, _V]),
@@ -242,6 +244,12 @@ class Modem:
 
     def int16_to_double(self, iq16, n: int, out, stream=None):
         check(lib().ofdm_int16_to_double(self.h, _ptr(iq16), n, _ptr(out), _stream(stream)))
+
+    def double_to_int16(self, iq, n: int, out16, stream=None):
+        check(lib().ofdm_double_to_int16(self.h, _ptr(iq), n, _ptr(out16), _stream(stream)))
+
+    def preamble_corr(self, iq, n: int, start: int, cor_out, stream=None):
+        check(lib().ofdm_preamble_corr(self.h, _ptr(iq), n, start, _ptr(cor_out), _stream(stream)))
 
     def t2_scan(self, iq, n: int, start: int, rel_out=None, first_out=None, stream=None):
         check(lib().ofdm_t2_scan(self.h, _ptr(iq), n, start, _ptr(rel_out), _ptr(first_out),

@@ -194,6 +194,10 @@ int ofdm_bit_convert(ofdm_ctx* ctx, const uint8_t* in, size_t len, int in_bits, 
  * samples -> n complex<double>. Device buffers. */
 int ofdm_int16_to_double(ofdm_ctx* ctx, const int16_t* in, size_t n, double* out, void* stream);
 
+/* FRAME_FORM::get_int16 (Frame.cpp:249-256) on n given samples:
+ * complex<int16>(x * complex(mult)) = per-component trunc(x*mult). Device buffers. */
+int ofdm_double_to_int16(ofdm_ctx* ctx, const double* in, size_t n, int16_t* out, void* stream);
+
 /* ---- rx sync front end ----------------------------- */
 /* T2SIN_FORM::corr (Frame.hpp:96-147) over all floor((n-start)/t2sin_size)
  * blocks from `start`: rel_out[b] = energy ratio if > level else 0 (device,
@@ -209,6 +213,12 @@ int ofdm_t2_scan(ofdm_ctx* ctx, const double* iq, size_t n, long start,
  * Samples past n read as 0. Device arrays. Callers add +1 (main.cpp:53). */
 int ofdm_find_preamble(ofdm_ctx* ctx, const double* iq, size_t n,
                        const int* starts, size_t nstarts, int* idx_out, void* stream);
+
+/* PREAMBLE_FORM::find_corr (Frame.cpp:297-335): the normalised correlation
+ * at every lag from `start` (cor_out[i] = |sum x[start+i+j] c_j| / sqrt(norm_i)
+ * where norm_i > 1, else 0; 2*T2sin_size + pr_sin_len lags). Device arrays. */
+int ofdm_preamble_corr(ofdm_ctx* ctx, const double* iq, size_t n, long start, double* cor_out,
+                       void* stream);
 
 /* ---- per-frame synchronisation, batched over located frames ------------
  * `x` points at the first sample of a form in frame 0; frame f's form starts

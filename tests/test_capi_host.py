@@ -90,3 +90,21 @@ def test_create_without_gpu_fails_loudly():
     with pytest.raises(M.OfdmError) as e:
         M.Modem(O.DEFAULT)
     assert e.value.code in (-3,)
+
+
+def test_reference_apps_build_unchanged_against_compat_headers():
+    """main.cpp / tx.cpp / rx.cpp of the reference compile and link against
+    c-ofdm_amd/compat/include + the MI355X library (oracle/Makefile `dropin`)."""
+    import subprocess
+    if not os.path.exists("/root/reference/main.cpp"):
+        pytest.skip("reference absent")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run(["make", "-s", "-C", os.path.join(root, "c-ofdm_amd")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    r = subprocess.run(["make", "-s", "-C", os.path.join(root, "oracle"), "dropin"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    for app in ("main", "tx", "rx"):
+        path = os.path.join(root, "oracle", "_ref", app)
+        assert os.access(path, os.X_OK)
+        ldd = subprocess.run(["ldd", path], capture_output=True, text=True).stdout
+        assert "libofdm_compat.so" in ldd and "not found" not in ldd
