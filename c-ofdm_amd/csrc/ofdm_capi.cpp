@@ -115,6 +115,8 @@ struct ofdm_ctx {
     int* d_data_slot = nullptr;
     int* d_pilot_bin = nullptr;
     int* d_bin_map = nullptr;
+    int* d_rx_pack = nullptr;
+    int* d_pilot_swz = nullptr;
     double2* d_const = nullptr;
     double2* d_const_bpsk = nullptr;
     double2* d_header = nullptr;   // T2 + preamble
@@ -146,6 +148,8 @@ struct ofdm_ctx {
         t.data_slot = d_data_slot;
         t.pilot_bin = d_pilot_bin;
         t.bin_map = d_bin_map;
+        t.rx_pack = d_rx_pack;
+        t.pilot_swz = d_pilot_swz;
         t.constell = bpsk ? d_const_bpsk : d_const;
         return t;
     }
@@ -270,7 +274,8 @@ int ofdm_destroy(ofdm_ctx* c)
 {
     if (!c) return OFDM_OK;
     (void)hipSetDevice(c->device);
-    void* ptrs[] = {c->d_tw, c->d_data_bin, c->d_data_slot, c->d_pilot_bin, c->d_bin_map, c->d_const,
+    void* ptrs[] = {c->d_tw, c->d_data_bin, c->d_data_slot, c->d_pilot_bin, c->d_bin_map, c->d_rx_pack,
+                    c->d_pilot_swz, c->d_const,
                     c->d_const_bpsk, c->d_header, c->d_preamble, c->d_templ, c->d_modpre, c->d_t2mask,
                     c->d_t2tw, c->d_first, c->d_scratch, c->d_cfo_scratch};
     for (void* q : ptrs)
@@ -376,7 +381,14 @@ int ofdm_create(const ofdm_params* params, int device, ofdm_ctx** out)
             }
         }
     }
-    if ((rc = upload(&c->d_tw, twiddles(c->N))) || (rc = upload(&c->d_data_bin, data_bin)) ||
+    // rx per-thread tables, zero-padded to the rx kernel's fixed per-thread
+    // counts (RX_DPT data and one pilot per thread) so it loads them unguarded
+    std::vector<int> rx_pack(std::max(c->D, ofdm::RX_DPT * (c->N / 8)), 0),
+        pilot_swz(std::max(c->P, c->N / 8), 0);
+    for (int d = 0; d < c->D; ++d) rx_pack[d] = ofdm::lds_swz_host(data_bin[d]) | (data_slot[d] << 16);
+    for (int j = 0; j < c->P; ++j) pilot_swz[j] = ofdm::lds_swz_host(pilot[j]);
+    if ((rc = upload(&c->d_rx_pack, rx_pack)) || (rc = upload(&c->d_pilot_swz, pilot_swz)) ||
+        (rc = upload(&c->d_tw, twiddles(c->N))) || (rc = upload(&c->d_data_bin, data_bin)) ||
         (rc = upload(&c->d_data_slot, data_slot)) || (rc = upload(&c->d_pilot_bin, pilot)) ||
         (rc = upload(&c->d_bin_map, bin_map)) || (rc = upload(&c->d_const, constellation(c->k))) ||
         (rc = upload(&c->d_const_bpsk, constellation(1)))) {

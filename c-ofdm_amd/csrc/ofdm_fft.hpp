@@ -98,13 +98,40 @@ __device__ __forceinline__ void load_twiddles(const double2* __restrict__ tw, do
                                               int nthreads)
 {
     constexpr int NHI = TwLds<LOGN>::NHI;
-    for (int i = t; i < NHI + 64; i += nthreads) {
+    for (int i = t; i < NHI + 64; i += nthreads) {  // branch-free body: loads are not serialised
         const int j = i - NHI;
-        if (i < NHI)
-            lds_tw[i] = tw[i * 64];
-        else
-            lds_tw[NHI + (j ^ ((j >> 4) & 3))] = tw[j];
+        const bool hi = i < NHI;
+        const double2 w = tw[hi ? i * 64 : j];
+        lds_tw[hi ? i : NHI + (j ^ ((j >> 4) & 3))] = w;
     }
+}
+
+// Split fill for kernels that must not wait on their own prefetch: fetch one
+// table entry per thread unconditionally (clamped), store it later. Needs
+// T >= TwLds::SIZE (N >= 1024); smaller N use load_twiddles.
+template <int LOGN>
+struct TwPiece {
+    double2 w;
+    int dst;
+};
+
+template <int LOGN>
+__device__ __forceinline__ TwPiece<LOGN> tw_fetch(const double2* __restrict__ tw, int t)
+{
+    constexpr int NHI = TwLds<LOGN>::NHI;
+    const int i = t < NHI + 64 ? t : 0;
+    const int j = i - NHI;
+    const bool hi = i < NHI;
+    return {tw[hi ? i * 64 : j], hi ? i : NHI + (j ^ ((j >> 4) & 3))};
+}
+
+// Unconditional: threads past the table rewrite entry 0 with the identical
+// value (a guarded store would let the compiler sink the load into the guard
+// and wait on every load issued before it).
+template <int LOGN>
+__device__ __forceinline__ void tw_store(const TwPiece<LOGN>& p, double2* __restrict__ lds_tw)
+{
+    lds_tw[p.dst] = p.w;
 }
 
 // W_N^j (forward sign) from the LDS table.
@@ -184,20 +211,15 @@ __device__ __forceinline__ void stockham_pass(double2 (&v)[8], int t, const doub
         if constexpr (NS > 1) {
             double2 w1 = tw_get<LOGN>(lds_tw, k * (N / (NS * R)));
             if (SIGN > 0) w1.y = -w1.y;
-            double2 w[8];
-            w[1] = w1;
-            if constexpr (R >= 4) {
-                w[2] = cmul(w1, w1);
-                w[3] = cmul(w[2], w1);
-            }
-            if constexpr (R == 8) {
-                w[4] = cmul(w[2], w[2]);
-                w[5] = cmul(w[4], w1);
-                w[6] = cmul(w[3], w[3]);
-                w[7] = cmul(w[4], w[3]);
-            }
+            // running power w^r (two live twiddles: the register window of the
+            // streaming kernels leaves no room for all seven)
+            double2 w = w1;
+            v[u + B] = cmul(v[u + B], w1);
 #pragma unroll
-            for (int r = 1; r < R; ++r) v[u + r * B] = cmul(v[u + r * B], w[r]);
+            for (int r = 2; r < R; ++r) {
+                w = cmul(w, w1);
+                v[u + r * B] = cmul(v[u + r * B], w);
+            }
         }
         if constexpr (R == 8)
             dft8<SIGN>(v[u], v[u + B], v[u + 2 * B], v[u + 3 * B], v[u + 4 * B], v[u + 5 * B],
@@ -207,8 +229,16 @@ __device__ __forceinline__ void stockham_pass(double2 (&v)[8], int t, const doub
         else
             dft2<SIGN>(v[u], v[u + B]);
         const int idxD = (b - k) * R + k;
+        if constexpr (NS % 64 == 0) {
+            // r*NS has zero low 6 bits: the swizzle of idxD carries over, so one
+            // base address + immediate offsets
+            double2* base = lds + lds_swz(idxD);
 #pragma unroll
-        for (int r = 0; r < R; ++r) lds[lds_swz(idxD + r * NS)] = v[u + r * B];
+            for (int r = 0; r < R; ++r) base[r * NS] = v[u + r * B];
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) lds[lds_swz(idxD + r * NS)] = v[u + r * B];
+        }
     }
 }
 
@@ -216,8 +246,14 @@ template <int LOGN>
 __device__ __forceinline__ void lds_load8(double2 (&v)[8], int t, const double2* __restrict__ lds)
 {
     constexpr int T = (1 << LOGN) / 8;
+    if constexpr (T % 64 == 0) {
+        const double2* base = lds + lds_swz(t);  // T*i has zero low 6 bits
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = lds[lds_swz(t + T * i)];
+        for (int i = 0; i < 8; ++i) v[i] = base[T * i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = lds[lds_swz(t + T * i)];
+    }
 }
 
 // Remaining passes after the first one has been written to `lds`.
@@ -249,6 +285,57 @@ __device__ __forceinline__ void fft_block(double2 (&v)[8], int t, const double2*
     stockham_pass<LOGN, 8, 1, SIGN>(v, t, lds_tw, lds);
     fft_tail<LOGN, 1, SIGN>(v, t, lds_tw, lds);
     lds_barrier();
+}
+
+// ---------------------------------------------------------------- ping-pong
+// Same transform over two LDS images: pass p writes buf[(start + p) & 1] and
+// pass p+1 reads it, so one barrier per pass suffices (a buffer is only
+// rewritten two passes later, after every thread has crossed the barrier that
+// follows its last read). Used by the streaming tx/rx kernels, where it halves
+// the per-symbol barriers of fft_block.
+template <int LOGN>
+struct FftPasses {
+    static constexpr int value = FftShape<LOGN>::NPASS8 + (FftShape<LOGN>::REM ? 1 : 0);
+};
+
+struct NoHook {
+    __device__ __forceinline__ void operator()() const {}
+};
+
+template <int LOGN, int PASS, int SIGN, class Hook>
+__device__ __forceinline__ void fft_pp_tail(double2 (&v)[8], int t, const double2* __restrict__ lds_tw,
+                                            double2* __restrict__ b0, double2* __restrict__ b1, const Hook& hook)
+{
+    using S = FftShape<LOGN>;
+    constexpr int NPASS = FftPasses<LOGN>::value;
+    if constexpr (PASS < NPASS) {
+        constexpr bool is8 = PASS < S::NPASS8;
+        constexpr int R = is8 ? 8 : (1 << S::REM);
+        constexpr int NS = 1 << (3 * PASS);
+        lds_barrier();  // pass PASS-1 fully written to b1
+        lds_load8<LOGN>(v, t, b1);
+        stockham_pass<LOGN, R, NS, SIGN>(v, t, lds_tw, b0);
+        fft_pp_tail<LOGN, PASS + 1, SIGN>(v, t, lds_tw, b1, b0, hook);
+    } else {
+        hook();         // e.g. publish the next symbol's LDS inputs under the same barrier
+        lds_barrier();  // result (in b1) visible
+    }
+}
+
+// On entry v[i] = x[t + T*i]. Pass 0 writes `first`; returns the buffer
+// holding the natural-order result (index lds_swz(k)), workgroup synced. A
+// caller that streams symbols passes the returned buffer as `second` (and the
+// other one as `first`) on the next call, so pass 0 never overwrites a buffer
+// other threads may still be reading.
+template <int LOGN, int SIGN, class Hook = NoHook>
+__device__ __forceinline__ double2* fft_pp(double2 (&v)[8], int t, const double2* __restrict__ lds_tw,
+                                           double2* __restrict__ first, double2* __restrict__ second,
+                                           const Hook& hook = Hook())
+{
+    static_assert(LOGN >= 6 && LOGN <= 12, "N must be 64..4096");
+    stockham_pass<LOGN, 8, 1, SIGN>(v, t, lds_tw, first);
+    fft_pp_tail<LOGN, 1, SIGN>(v, t, lds_tw, second, first, hook);
+    return (FftPasses<LOGN>::value & 1) ? first : second;
 }
 
 }  // namespace ofdm

@@ -13,6 +13,8 @@ struct DevTables {
     const int* data_slot;       // D: pilot slot j = d / seg owning data index d
     const int* pilot_bin;       // P
     const int* bin_map;         // N: >=0 data index, -1 unused bin, -2 pilot
+    const int* rx_pack;         // max(D, RX_DPT*N/8): lds_swz(data_bin) | data_slot << 16, 0-padded
+    const int* pilot_swz;       // max(P, N/8): lds_swz(pilot_bin), 0-padded
     const double2* constell;    // 2^k mapping table (Modulation::constell)
 };
 
@@ -68,6 +70,8 @@ hipError_t launch_f64_to_i16(const double* in, long n, double mult, int16_t* out
 
 // Register-resident rx limits: S*ceil(D/T) <= RX_REG_SLOTS.
 constexpr int RX_SMAX = 8;
+// LDS slot of FFT element e (ofdm_fft.hpp lds_swz), for host-built tables
+inline int lds_swz_host(int e) { return e ^ ((e >> 3) & 7); }
 constexpr int RX_DPT = 4;
 // tx: persistent grid-stride launch size (symbols per workgroup = nsym / grid)
 constexpr long TX_MAX_GRID = 4096;

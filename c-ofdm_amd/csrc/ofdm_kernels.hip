@@ -56,23 +56,40 @@ __device__ __forceinline__ double2 clamp_point(double2 z)
                         z.y < -1.0 ? -1.0 : (1.0 < z.y ? 1.0 : z.y));
 }
 
-__device__ __forceinline__ uint64_t mix64(uint64_t z)
+// 32-bit integer hash (lowbias32: two 32-bit multiplies; full 64-bit mixers
+// cost ~4x more quarter-rate v_mul per sample).
+__device__ __forceinline__ uint32_t lowbias32(uint32_t x)
 {
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+
+// Per-seed keys of the AWGN counter hash.
+struct AwgnKey {
+    uint32_t k0, k1;
+};
+
+__device__ __forceinline__ AwgnKey awgn_key(unsigned long long seed)
+{
+    const uint32_t k0 = lowbias32((uint32_t)seed ^ 0x9E3779B9u);
+    return {k0, lowbias32((uint32_t)(seed >> 32) + k0)};
 }
 
 // Counter-based Box-Muller AWGN (same definition as oracle orc_awgn). A
-// channel model, not modem arithmetic: 24-bit uniforms and the gfx950 FP32
-// transcendental units (v_log_f32 = log2, v_sin/cos_f32 take revolutions),
-// ~10 VALU ops per sample instead of an FP64 log/sqrt/sincos (~200).
-__device__ __forceinline__ double2 awgn_sample(unsigned long long seed, unsigned long long g, double sc)
+// channel model, not modem arithmetic: sample g's two 24-bit uniforms come
+// from h1 = H(H(lo(g) ^ k0) + (hi(g) ^ k1)), h2 = H(h1 ^ c); log/sin/cos run on
+// the gfx950 FP32 transcendental units (v_log_f32 = log2, v_sin/cos_f32 take
+// revolutions).
+__device__ __forceinline__ double2 awgn_sample(AwgnKey key, unsigned long long g, double sc)
 {
-    const uint64_t h1 = mix64(seed + 0x9E3779B97F4A7C15ull * (2 * g + 1));
-    const uint64_t h2 = mix64(seed + 0x9E3779B97F4A7C15ull * (2 * g + 2));
-    const float u1 = (float)((h1 >> 40) + 1) * 0x1.0p-24f;  // (0, 1]
-    const float u2 = (float)(h2 >> 40) * 0x1.0p-24f;        // [0, 1)
+    const uint32_t h1 = lowbias32(lowbias32((uint32_t)g ^ key.k0) + ((uint32_t)(g >> 32) ^ key.k1));
+    const uint32_t h2 = lowbias32(h1 ^ 0x632BE5ABu);
+    const float u1 = (float)((h1 >> 8) + 1) * 0x1.0p-24f;  // (0, 1]
+    const float u2 = (float)(h2 >> 8) * 0x1.0p-24f;        // [0, 1)
     const float r = __builtin_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));  // sqrt(-2 ln u1)
     const float c = __builtin_amdgcn_cosf(u2), s = __builtin_amdgcn_sinf(u2);           // of 2*pi*u2
     return make_double2((double)(r * c) * sc, (double)(r * s) * sc);
@@ -167,9 +184,12 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) tx_kernel(TxArgs a)
     }
     lds_barrier();  // twiddle table + first payload visible
 
+    // (frame, symbol) of `sym`, advanced incrementally (no 64-bit division in the loop)
+    const long gstep_f = gridDim.x / a.S;
+    const int gstep_s = (int)(gridDim.x - gstep_f * a.S);
+    long f = sym / a.S;
+    int s = (int)(sym - f * a.S);
     for (; sym < nsym; sym += gridDim.x) {
-        const long f = sym / a.S;
-        const int s = (int)(sym - f * a.S);
         // Modulation::mod: k-bit symbol -> constellation point (modulation.cpp:39-50)
         double2 v[8];
 #pragma unroll
@@ -193,12 +213,22 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) tx_kernel(TxArgs a)
         }
 
         fft_block<LOGN, +1>(v, t, lds_tw, fft);
+        // Publish the next payload now, before this symbol's stores: on gfx9
+        // vmcnt also counts stores, so a wait on these loads placed after the
+        // stores would drain them every symbol. Every thread has mapped this
+        // symbol (FFT barriers since), so the single stage can be rewritten.
+        if constexpr (!POINTS) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+                if (t + T * r < bps) sbytes[t + T * r] = nb[r];
+        }
 
         // body / sqrt(N) after a CP copy of its last cp samples (Frame.cpp:66-68,191-197)
         const long base = f * a.frame_stride + a.msg_offset + (long)s * L;
         double2* out = a.iq + base;
         int16_t* out16 = a.iq16 ? a.iq16 + 2 * base : nullptr;
         const unsigned long long g0 = a.sample_offset + (unsigned long long)sym * L;
+        const AwgnKey key = awgn_key(a.seed);
         for (int j = t; j < L; j += T) {
             const int n = j < a.cp ? N - a.cp + j : j - a.cp;
             double2 z = fft[lds_swz(n)];
@@ -209,7 +239,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) tx_kernel(TxArgs a)
                 out16[2 * j + 1] = to_int16(z.y * a.mult);
             }
             if (a.noise_scale > 0.0) {
-                const double2 w = awgn_sample(a.seed, g0 + j, a.noise_scale);
+                const double2 w = awgn_sample(key, g0 + j, a.noise_scale);
                 z.x += w.x;
                 z.y += w.y;
             }
@@ -228,51 +258,30 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) tx_kernel(TxArgs a)
                 }
             }
         }
-        if constexpr (!POINTS) {
-#pragma unroll
-            for (int r = 0; r < 8; ++r)
-                if (t + T * r < bps) sbytes[t + T * r] = nb[r];
-        }
         lds_barrier();  // next payload visible; fft[] output reads precede the next pass 0
+        s += gstep_s;
+        f += gstep_f;
+        if (s >= a.S) {
+            s -= a.S;
+            ++f;
+        }
     }
 }
 
 // ------------------------------------------------------------------ rx
-// One workgroup per frame. Symbol s+1 streams HBM -> LDS stage by LDS-DMA
-// (global_load_lds_dwordx4) while symbol s is transformed, so the load of the
-// next symbol overlaps the FFT with no extra VGPRs.
+// One workgroup per frame. Symbol s+1 is loaded into registers (8 x 16 B per
+// thread, coalesced) while symbol s is transformed; the FFT ping-pongs
+// between two LDS images (fft_pp: one barrier per pass, no input stage).
 // STAGED=false: the frame's S*D equalisation inputs live in VGPRs
-//   (S <= RX_SMAX, D <= RX_DPT*T); a rolled symbol loop shifts them through a
-//   fixed register window so every register index stays compile-time.
+//   (S <= RX_SMAX, D <= RX_DPT*T), written through a wave-uniform switch on
+//   the symbol index so every register index is compile-time.
 // STAGED=true: any S; inputs parked in a.ystage (same-thread re-read).
-// The DMA is issued through inline asm (MI355X guide §5.7 LDS-DMA recipe:
-// save M0, M0 = wave-uniform LDS byte address, global_load_lds_dwordx4,
-// restore M0). hipcc cannot prove the stage and the FFT buffer disjoint and
-// would otherwise wait vmcnt(0) before the first FFT ds_write, draining the
-// prefetch; the kernel's own `s_waitcnt vmcnt(0)` before reading the stage is
-// the only wait the DMA needs (no other vector-memory ops are in flight then).
 template <int LOGN>
-__device__ __forceinline__ void dma_symbol(const double2* __restrict__ src, double2* stage, int t)
+__device__ __forceinline__ void load_symbol(double2 (&r)[8], const double2* __restrict__ src, int t)
 {
     constexpr int T = (1 << LOGN) / 8;
-    const int w0 = t & ~63;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int e0 = w0 + T * i;  // wave-uniform: the wave's 64 lanes land contiguously
-        const double2* g = src + e0 + (t & 63);
-        const unsigned lds = __builtin_amdgcn_readfirstlane(
-            (unsigned)(uintptr_t)(__attribute__((address_space(3))) double2*)(stage + e0));
-        unsigned keep;
-        asm volatile(
-            "s_mov_b32 %0, m0\n\t"
-            "s_mov_b32 m0, %2\n\t"
-            "s_nop 0\n\t"
-            "global_load_lds_dwordx4 %1, off\n\t"
-            "s_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "v"(g), "s"(lds)
-            : "memory");
-    }
+    for (int i = 0; i < 8; ++i) r[i] = src[t + T * i];
 }
 
 template <int LOGN, bool STAGED>
@@ -283,59 +292,77 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
     constexpr int SW = STAGED ? 1 : RX_SMAX;  // register window (symbols)
     extern __shared__ double2 smem[];
     const int S = a.S, D = a.D, P = a.P;
-    double2* stage = smem;                  // N raw samples (DMA target)
-    double2* fft = stage + N;               // PADN
-    double2* lds_tw = fft + FS::PADN;       // TwLds::SIZE
+    double2* bufA = smem;                   // FFT ping-pong images
+    double2* bufB = bufA + N;
+    double2* lds_tw = bufB + FS::PADN;      // TwLds::SIZE
     double2* pil = lds_tw + TwLds<LOGN>::SIZE;  // S*P raw pilots
     double2* gain = pil + S * P;            // S*P equaliser gains
     double* red = reinterpret_cast<double*>(gain + S * P);
-    uint8_t* dec = reinterpret_cast<uint8_t*>(fft);  // aliases fft after the transforms
+    uint8_t* dec = reinterpret_cast<uint8_t*>(bufA);  // aliases the FFT images after the transforms
 
     const int t = threadIdx.x;
     const long f = blockIdx.x;
     const int L = N + a.cp;
     const double2* x = a.iq + f * a.frame_stride + a.cp;  // CP strip (Frame.hpp:278-279)
 
-    dma_symbol<LOGN>(x, stage, t);
-    load_twiddles<LOGN>(a.tab.tw, lds_tw, t, T);
-    int bins[RX_DPT], slot[RX_DPT];
+    // table loads first, then symbol 0: every prologue wait below is a
+    // counted vmcnt that leaves the symbol prefetch in flight
+    constexpr bool kTwSplit = T >= TwLds<LOGN>::SIZE;
+    TwPiece<LOGN> twp{};
+    if constexpr (kTwSplit)
+        twp = tw_fetch<LOGN>(a.tab.tw, t);
+    else
+        load_twiddles<LOGN>(a.tab.tw, lds_tw, t, T);
+    // data carrier d = t + T*i: swizzled LDS slot of its FFT bin (low 16 bits)
+    // | pilot slot (high 16); host tables are zero-padded, so no guards here
+    int pk[RX_DPT];
 #pragma unroll
-    for (int i = 0; i < RX_DPT; ++i) {
-        const int d = t + T * i;
-        bins[i] = d < D ? a.tab.data_bin[d] : 0;
-        slot[i] = d < D ? a.tab.data_slot[d] : 0;
-    }
-    const int pbin = t < P ? a.tab.pilot_bin[t] : 0;
+    for (int i = 0; i < RX_DPT; ++i) pk[i] = a.tab.rx_pack[t + T * i];
+    const int pbin = a.tab.pilot_swz[t];
+    double2 pf[8];
+    load_symbol<LOGN>(pf, x, t);
+    if constexpr (kTwSplit) tw_store<LOGN>(twp, lds_tw);  // read after pass 0's barrier
 
     double2 y[SW][RX_DPT];
+    double2* first = bufA;
+    double2* second = bufB;
 #pragma unroll 1
     for (int s = 0; s < S; ++s) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of symbol s landed
-        lds_barrier();                                     // ... and every other wave's
         double2 v[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = stage[t + T * i];
-        lds_barrier();  // stage fully read: refill it with symbol s+1
-        if (s + 1 < S) dma_symbol<LOGN>(x + (long)(s + 1) * L, stage, t);
-        fft_block<LOGN, -1>(v, t, lds_tw, fft);
-        if (t < P) pil[s * P + t] = fft[lds_swz(pbin)];
+        for (int i = 0; i < 8; ++i) v[i] = pf[i];
+        if (s + 1 < S) load_symbol<LOGN>(pf, x + (long)(s + 1) * L, t);
+        // opaque copy of t: the per-pass LDS addresses are recomputed each
+        // symbol instead of being hoisted out of the loop and held live
+        // beside the register window
+        int tl;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(tl) : "v"(t));
+        double2* res = fft_pp<LOGN, -1>(v, tl, lds_tw, first, second);
+        first = res == bufA ? bufB : bufA;
+        second = res;
+        if (t < P) pil[s * P + t] = res[pbin];
         if constexpr (STAGED) {
 #pragma unroll
             for (int i = 0; i < RX_DPT; ++i) {
                 const int d = t + T * i;
-                if (d < D) a.ystage[(f * S + s) * D + d] = fft[lds_swz(bins[i])];
+                if (d < D) a.ystage[(f * S + s) * D + d] = res[pk[i] & 0xffff];
             }
         } else {
-#pragma unroll
-            for (int w = 0; w < SW - 1; ++w)
-#pragma unroll
-                for (int i = 0; i < RX_DPT; ++i) y[w][i] = y[w + 1][i];
-#pragma unroll
-            for (int i = 0; i < RX_DPT; ++i) y[SW - 1][i] = fft[lds_swz(bins[i])];
+            switch (s) {
+#define OFDM_RX_PUT(W)                                                                    \
+    case W:                                                                               \
+        if constexpr (W < SW) {                                                           \
+            _Pragma("unroll") for (int i = 0; i < RX_DPT; ++i) y[W][i] = res[pk[i] & 0xffff]; \
+        }                                                                                 \
+        break;
+                OFDM_RX_PUT(0) OFDM_RX_PUT(1) OFDM_RX_PUT(2) OFDM_RX_PUT(3)
+                OFDM_RX_PUT(4) OFDM_RX_PUT(5) OFDM_RX_PUT(6) OFDM_RX_PUT(7)
+#undef OFDM_RX_PUT
+                default: break;
+            }
         }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();
+    lds_barrier();  // pilots of the last symbol visible
 
     // phys_pilot_ampl = sum |pilot| / (P*S*pilot_ampl)   (Frame.cpp:76-80)
     double acc = 0.0;
@@ -361,7 +388,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
 
     auto emit = [&](int s, int i, double2 yv) {
         const int d = t + T * i;
-        double2 o = cmul_exact(yv, gain[s * P + slot[i]]);
+        double2 o = cmul_exact(yv, gain[s * P + (pk[i] >> 16)]);
         if (chan) o = cdiv_exact(o, chan[d]);
         if (a.constell) a.constell[(f * S + s) * D + d] = o;
         dec[whole_frame_dec ? s * D + d : d] = (uint8_t)decide(o, a.k, s1, m);
@@ -392,11 +419,10 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
     if constexpr (!STAGED) {
 #pragma unroll
         for (int w = 0; w < SW; ++w) {
-            const int s = w - (SW - S);
-            if (s >= 0) {
+            if (w < S) {
 #pragma unroll
                 for (int i = 0; i < RX_DPT; ++i)
-                    if (t + T * i < D) emit(s, i, y[w][i]);
+                    if (t + T * i < D) emit(w, i, y[w][i]);
             }
         }
         __syncthreads();

@@ -720,27 +720,34 @@ void orc_get_int16(const double* xd, long n, long mult, int16_t* out)
 /* Loopback channel + batched drivers (bench cpu_baseline)                   */
 /* ------------------------------------------------------------------------ */
 
-static inline uint64_t mix64(uint64_t z)
+static inline uint32_t lowbias32(uint32_t x)
 {
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
 }
 
-/* Counter-based Box-Muller AWGN; same definition as the HIP tx kernel (24-bit
- * uniforms from splitmix64 of the sample counter). The GPU evaluates log/sin/
- * cos on its FP32 units, so the two agree to ~1e-6 of noise_std, not bitwise. */
+/* Counter-based Box-Muller AWGN; same definition as the HIP tx kernel
+ * (ofdm_kernels.hip awgn_sample): 24-bit uniforms from a lowbias32 hash of the
+ * 64-bit sample counter and seed. The GPU evaluates log/sin/cos on its FP32
+ * units, so the two agree to ~1e-6 of noise_std, not bitwise. A channel model
+ * of this repo (the reference's channel is the radio, python_code/channel.py). */
 void orc_awgn(double* xd, long n, double noise_std, unsigned long long seed,
               unsigned long long off)
 {
     cplx* x = (cplx*)xd;
     double sc = noise_std * M_SQRT1_2;
+    const uint32_t k0 = lowbias32((uint32_t)seed ^ 0x9E3779B9u);
+    const uint32_t k1 = lowbias32((uint32_t)(seed >> 32) + k0);
     for (long i = 0; i < n; i++) {
         uint64_t g = off + (uint64_t)i;
-        uint64_t h1 = mix64(seed + 0x9E3779B97F4A7C15ull * (2 * g + 1));
-        uint64_t h2 = mix64(seed + 0x9E3779B97F4A7C15ull * (2 * g + 2));
-        double u1 = (double)(float)((float)((h1 >> 40) + 1) * 0x1.0p-24f);
-        double u2 = (double)(float)((float)(h2 >> 40) * 0x1.0p-24f);
+        uint32_t h1 = lowbias32(lowbias32((uint32_t)g ^ k0) + ((uint32_t)(g >> 32) ^ k1));
+        uint32_t h2 = lowbias32(h1 ^ 0x632BE5ABu);
+        double u1 = (double)(float)((float)((h1 >> 8) + 1) * 0x1.0p-24f);
+        double u2 = (double)(float)((float)(h2 >> 8) * 0x1.0p-24f);
         double r = sqrt(-2.0 * log(u1)) * sc;
         double th = 2.0 * M_PI * u2;
         x[i] += CMPLX(r * cos(th), r * sin(th));
