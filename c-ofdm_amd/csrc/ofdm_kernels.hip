@@ -81,21 +81,51 @@ __device__ __forceinline__ AwgnKey awgn_key(unsigned long long seed)
 
 // Counter-based Box-Muller AWGN (same definition as oracle orc_awgn). A
 // channel model, not modem arithmetic: sample g's two 24-bit uniforms come
-// from h1 = H(H(lo(g) ^ k0) + (hi(g) ^ k1)), h2 = H(h1 ^ c); log/sin/cos run on
-// the gfx950 FP32 transcendental units (v_log_f32 = log2, v_sin/cos_f32 take
-// revolutions).
-__device__ __forceinline__ double2 awgn_sample(AwgnKey key, unsigned long long g, double sc)
+// from h1 = H(lo(g) ^ K(hi(g))), K(h) = H(h ^ k1) ^ k0, and h2 = H(h1 ^ c)
+// (H = lowbias32); log/sqrt/sin/cos run on the gfx950 FP32 transcendental
+// units (v_log_f32 = log2, v_sin/cos_f32 take revolutions).
+// Per run of samples from g0 (< 2^32 long) the two possible K values are
+// computed once and selected on low-word wrap.
+struct AwgnRun {
+    uint32_t lo0, ka, kb;  // lo(g0), K(hi(g0)), K(hi(g0) + 1)
+};
+
+__device__ __forceinline__ AwgnRun awgn_run(AwgnKey key, unsigned long long g0)
 {
-    const uint32_t h1 = lowbias32(lowbias32((uint32_t)g ^ key.k0) + ((uint32_t)(g >> 32) ^ key.k1));
+    const uint32_t hi = (uint32_t)(g0 >> 32);
+    return {(uint32_t)g0, lowbias32(hi ^ key.k1) ^ key.k0, lowbias32((hi + 1u) ^ key.k1) ^ key.k0};
+}
+
+__device__ __forceinline__ double2 awgn_sample(const AwgnRun& run, uint32_t j, double sc)
+{
+    const uint32_t lo = run.lo0 + j;
+    const uint32_t h1 = lowbias32(lo ^ (lo < run.lo0 ? run.kb : run.ka));
     const uint32_t h2 = lowbias32(h1 ^ 0x632BE5ABu);
     const float u1 = (float)((h1 >> 8) + 1) * 0x1.0p-24f;  // (0, 1]
     const float u2 = (float)(h2 >> 8) * 0x1.0p-24f;        // [0, 1)
-    const float r = __builtin_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));  // sqrt(-2 ln u1)
-    const float c = __builtin_amdgcn_cosf(u2), s = __builtin_amdgcn_sinf(u2);           // of 2*pi*u2
+    const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));  // sqrt(-2 ln u1)
+    const float c = __builtin_amdgcn_cosf(u2), s = __builtin_amdgcn_sinf(u2);                  // of 2*pi*u2
     return make_double2((double)(r * c) * sc, (double)(r * s) * sc);
 }
 
 __device__ __forceinline__ int16_t to_int16(double v) { return (int16_t)(int)v; }
+
+// Streams touched once (tx output, rx input, constellation output): non-temporal
+// 16-B accesses, so a launch neither evicts the caches for nothing nor leaves
+// gigabytes of dirty lines for the next launch to write back.
+typedef double nt_double2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void store_nt(double2* p, double2 v)
+{
+    nt_double2 w = {v.x, v.y};
+    __builtin_nontemporal_store(w, reinterpret_cast<nt_double2*>(p));
+}
+
+__device__ __forceinline__ double2 load_nt(const double2* p)
+{
+    const nt_double2 w = __builtin_nontemporal_load(reinterpret_cast<const nt_double2*>(p));
+    return make_double2(w.x, w.y);
+}
 
 template <int NT>
 __device__ __forceinline__ double block_sum(double v, double* red)
@@ -228,22 +258,22 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) tx_kernel(TxArgs a)
         double2* out = a.iq + base;
         int16_t* out16 = a.iq16 ? a.iq16 + 2 * base : nullptr;
         const unsigned long long g0 = a.sample_offset + (unsigned long long)sym * L;
-        const AwgnKey key = awgn_key(a.seed);
+        const AwgnRun run = awgn_run(awgn_key(a.seed), g0);
         for (int j = t; j < L; j += T) {
             const int n = j < a.cp ? N - a.cp + j : j - a.cp;
             double2 z = fft[lds_swz(n)];
             z.x *= a.inv_sqrt_n;
             z.y *= a.inv_sqrt_n;
             if (out16) {
-                out16[2 * j] = to_int16(z.x * a.mult);
-                out16[2 * j + 1] = to_int16(z.y * a.mult);
+                const uint32_t w = (uint16_t)to_int16(z.x * a.mult) | ((uint32_t)(uint16_t)to_int16(z.y * a.mult) << 16);
+                __builtin_nontemporal_store(w, reinterpret_cast<uint32_t*>(out16 + 2 * j));
             }
             if (a.noise_scale > 0.0) {
-                const double2 w = awgn_sample(key, g0 + j, a.noise_scale);
+                const double2 w = awgn_sample(run, (uint32_t)j, a.noise_scale);
                 z.x += w.x;
                 z.y += w.y;
             }
-            out[j] = z;
+            store_nt(out + j, z);
         }
         // [T2 | preamble] header of full FRAME_FORM buffers (Frame.cpp:219,228-229)
         if (a.header && s == 0) {
@@ -281,7 +311,7 @@ __device__ __forceinline__ void load_symbol(double2 (&r)[8], const double2* __re
 {
     constexpr int T = (1 << LOGN) / 8;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) r[i] = src[t + T * i];
+    for (int i = 0; i < 8; ++i) r[i] = load_nt(src + t + T * i);
 }
 
 template <int LOGN, bool STAGED>
@@ -390,7 +420,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
         const int d = t + T * i;
         double2 o = cmul_exact(yv, gain[s * P + (pk[i] >> 16)]);
         if (chan) o = cdiv_exact(o, chan[d]);
-        if (a.constell) a.constell[(f * S + s) * D + d] = o;
+        if (a.constell) store_nt(a.constell + (f * S + s) * D + d, o);
         dec[whole_frame_dec ? s * D + d : d] = (uint8_t)decide(o, a.k, s1, m);
     };
 

@@ -744,7 +744,7 @@ void orc_awgn(double* xd, long n, double noise_std, unsigned long long seed,
     const uint32_t k1 = lowbias32((uint32_t)(seed >> 32) + k0);
     for (long i = 0; i < n; i++) {
         uint64_t g = off + (uint64_t)i;
-        uint32_t h1 = lowbias32(lowbias32((uint32_t)g ^ k0) + ((uint32_t)(g >> 32) ^ k1));
+        uint32_t h1 = lowbias32((uint32_t)g ^ lowbias32((uint32_t)(g >> 32) ^ k1) ^ k0);
         uint32_t h2 = lowbias32(h1 ^ 0x632BE5ABu);
         double u1 = (double)(float)((float)((h1 >> 8) + 1) * 0x1.0p-24f);
         double u2 = (double)(float)((float)(h2 >> 8) * 0x1.0p-24f);

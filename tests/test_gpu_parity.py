@@ -217,6 +217,24 @@ def test_full_size_loopback_config_b():
     assert rel_err(h[0], noisy) < 1e-5  # FP32 transcendental noise (channel model) vs FP64 oracle
 
 
+def test_awgn_counter_crosses_2_32_boundary():
+    """The fused channel noise is a function of (seed, global sample index) only:
+    frames whose sample counter wraps the low 32-bit word, with a seed using its
+    high word, match the oracle's counter definition (orc_awgn)."""
+    m = modem("B")
+    g = O.geometry(B)
+    nf = 3
+    data = payload(nf * g["bytes_per_frame"], seed=31)
+    off = (1 << 32) - g["message_len"] - 777  # frame 1 holds the wrap
+    seed = (7 << 40) + 12345
+    iq = torch.empty((nf * g["message_len"],), dtype=torch.complex128, device="cuda")
+    m.tx(dev(data), nf, iq, noise_std=0.3, seed=seed, sample_offset=off)
+    clean = O.tx_batch(B, data, nf)
+    want = O.awgn(clean, 0.3, seed=seed, sample_offset=off)
+    got = host(iq)
+    assert rel_err(got - clean, want - clean) < 1e-5  # FP32 transcendentals vs FP64 oracle
+
+
 def test_full_size_config_c_roundtrip():
     m = modem("C")
     g = O.geometry(CC)

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--configs", default="B,C,D")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--samples", type=float, default=1.68e8, help="target IQ samples per launch")
+    ap.add_argument("--alt", action="store_true", help="also time tx->rx alternating pairs")
     args = ap.parse_args()
     import torch
     import ofdm_mi355x as M
@@ -53,6 +54,26 @@ def main():
                                                    bit_errors=errs), rx_b + nf * S * D * k // 8),
             "rx(bytes)": (lambda: m.rx(iq, nf, bytes_out=out), nf * S * (16 * N + D * k // 8)),
         }
+        # alternating tx -> rx (the bench step): time each kernel of the pair
+        def alt(noise):
+            ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.reps)]
+            for _ in range(3):
+                m.tx(data, nf, iq, noise_std=noise, seed=1)
+                m.rx(iq, nf, constell_out=cons, bytes_out=out, ref=data, bit_errors=errs)
+            for e in ev:
+                e[0].record(st)
+                m.tx(data, nf, iq, noise_std=noise, seed=1)
+                e[1].record(st)
+                m.rx(iq, nf, constell_out=cons, bytes_out=out, ref=data, bit_errors=errs)
+                e[2].record(st)
+            torch.cuda.synchronize()
+            return (float(np.median([e[0].elapsed_time(e[1]) for e in ev])),
+                    float(np.median([e[1].elapsed_time(e[2]) for e in ev])))
+        if args.alt:
+            for noise in (0.0, 0.4):
+                txm, rxm = alt(noise)
+                print(json.dumps({"config": name, "variant": f"alt tx{'+awgn' if noise else ''} -> rx",
+                                  "tx_ms": round(txm, 4), "rx_ms": round(rxm, 4)}), flush=True)
         for vname, (fn, nbytes) in variants.items():
             for _ in range(3):
                 fn()

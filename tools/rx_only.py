@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""rx_only.py — run tx once and the rx kernel a few times at the bench workload
-(config B, 8192 frames), for rocprofv3 counter passes on the rx kernel alone."""
+"""rx_only.py — run the tx (with AWGN) and rx kernels a few times each at the
+bench workload (config B, 8192 frames), for rocprofv3 counter passes."""
 import os
 import sys
 
@@ -22,7 +22,8 @@ def main():
     cons = torch.empty((nf * CONFIG_B["num_data_subc"] * CONFIG_B["num_symb"],), dtype=torch.complex128, device="cuda")
     out = torch.empty_like(data)
     errs = torch.zeros((1,), dtype=torch.int64, device="cuda")
-    m.tx(data, nf, iq, noise_std=0.447, seed=1)
+    for _ in range(reps):
+        m.tx(data, nf, iq, noise_std=0.447, seed=1)
     for _ in range(reps):
         m.rx(iq, nf, constell_out=cons, bytes_out=out, ref=data, bit_errors=errs)
     torch.cuda.synchronize()

@@ -2,7 +2,6 @@
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out/sq
-rocprofv3 --list-avail > $R/gpurun_out/sq/avail.txt 2>&1 || true
 i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
            "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS" \
@@ -17,8 +16,9 @@ import csv, glob, collections
 acc = collections.defaultdict(list)
 for f in sorted(glob.glob("gpurun_out/sq/p*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        if "rx_kernel" in r["Kernel_Name"]:
-            acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
-for k, v in acc.items():
-    print(f"{k:28s} n={len(v)} mean={sum(v)/len(v):.6g}")
+        for kn in ("rx_kernel", "tx_kernel"):
+            if kn in r["Kernel_Name"] and int(r["Grid_Size"]) > 100000:
+                acc[(kn, r["Counter_Name"])].append(float(r["Counter_Value"]))
+for (kn, k), v in sorted(acc.items()):
+    print(f"{kn:10s} {k:28s} n={len(v)} mean={sum(v)/len(v):.6g}")
 PY
