@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cctype>
 #include <cmath>
 #include <complex>
@@ -139,6 +140,13 @@ struct ofdm_ctx {
     // staged-rx scratch (grown on demand, only for num_symb > 8 or D > N/2)
     double2* d_scratch = nullptr;
     size_t scratch_bytes = 0;
+    // ofdm_rx_stream scratch (grown on demand): walker records, frame batch,
+    // channel estimates, frame starts
+    struct Grow {
+        void* p = nullptr;
+        size_t bytes = 0;
+    };
+    Grow s_walk, s_batch, s_chan, s_pbs;
 
     ofdm::DevTables tables(bool bpsk) const
     {
@@ -280,6 +288,8 @@ int ofdm_destroy(ofdm_ctx* c)
                     c->d_t2tw, c->d_first, c->d_scratch, c->d_cfo_scratch};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
+    for (auto* g : {&c->s_walk, &c->s_batch, &c->s_chan, &c->s_pbs})
+        if (g->p) (void)hipFree(g->p);
     for (auto& pl : c->cfo_plans) {
         if (pl.tw_sub) (void)hipFree(pl.tw_sub);
         if (pl.tw_full) (void)hipFree(pl.tw_full);
@@ -618,6 +628,19 @@ int ofdm_stream_synchronize(ofdm_ctx* c, void* st)
 }
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// Device scratch that only grows (contents not preserved).
+static int grow(ofdm_ctx* c, ofdm_ctx::Grow& g, size_t need)
+{
+    if (need <= g.bytes) return OFDM_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    if (g.p) HIP_TRY(hipFree(g.p));
+    g.p = nullptr;
+    g.bytes = 0;
+    HIP_TRY(hipMalloc(&g.p, need));
+    g.bytes = need;
+    return OFDM_OK;
+}
 
 static void fill_tx(const ofdm_ctx* c, ofdm::TxArgs& a, const uint8_t* bytes, size_t nframes, double* iq,
                     size_t stride, int16_t* iq16, const ofdm_channel* ch)
@@ -1012,6 +1035,152 @@ int ofdm_sync_frames(ofdm_ctx* c, double* frames, size_t nframes, size_t stride,
     if ((stages & OFDM_SYNC_CHAN) && chan_out &&
         (rc = ofdm_chan_estimate(c, frames, nframes, stride, chan_out, (size_t)c->D, stream)))
         return rc;
+    return OFDM_OK;
+}
+
+int ofdm_rx_stream(ofdm_ctx* c, const double* iq, size_t n, size_t max_frames, long chunk, long* pb_out,
+                   uint8_t* bytes_out, double* constell_out, double* cfo_out, size_t* nframes_out, void* stream)
+{
+    if (!c || !iq || !nframes_out) return fail(OFDM_ERR_INVALID, "null argument");
+    *nframes_out = 0;
+    if (c->t2_logn < 6 || c->t2_logn > 11) return fail(OFDM_ERR_UNSUPPORTED, "stream walk needs T2sin_size = 2^a, 64..2048");
+    if (!aligned16(iq) || (constell_out && !aligned16(constell_out)))
+        return fail(OFDM_ERR_INVALID, "complex buffers must be 16-byte aligned");
+    if (n > (size_t)1 << 40) return fail(OFDM_ERR_INVALID, "stream too long");
+    hipStream_t st = (hipStream_t)stream;
+    const long L = c->L, pre = (long)L * c->npr, msg = (long)L * c->S, span = pre + msg;
+    const long flen = c->geo.frame_len, nn = (long)n;
+    if (nn == 0) return OFDM_OK;
+    // walkers: at most 4096 chunks, each >= 8 frames; halo of 3 frames to meet the true walk
+    if (chunk <= 0) chunk = std::max(8 * flen, (nn + 4095) / 4096);
+    chunk = std::max(chunk, (long)c->t2);
+    const long halo = 3 * flen;
+    const long nchunks = (nn + chunk - 1) / chunk;
+    if (nchunks > 1 << 20) return fail(OFDM_ERR_INVALID, "chunk too small for this stream");
+    // each located frame advances the walk by > message_len, and a walker can
+    // overshoot its core end by one scan step (256 threads x 8 samples) plus
+    // the preamble window: this many records always suffice
+    const int max_rec = (int)((chunk + halo + 2048 + 2 * c->p.t2sin_size + c->p.pr_sin_len) / msg + 4);
+    int rc;
+    const size_t rec_b = (size_t)nchunks * max_rec * sizeof(long);
+    const size_t walk_b = rec_b + (size_t)nchunks * (sizeof(long) + sizeof(int)) + 2 * sizeof(long) + 64;
+    if ((rc = grow(c, c->s_walk, walk_b))) return rc;
+    char* wb = static_cast<char*>(c->s_walk.p);
+    long* d_rec = reinterpret_cast<long*>(wb);
+    long* d_exit = reinterpret_cast<long*>(wb + rec_b);
+    long* d_start = d_exit + nchunks;  // one re-walk start
+    int* d_nrec = reinterpret_cast<int*>(d_start + 2);
+    int* d_ids = d_nrec + nchunks;     // one re-walk chunk id (in the 64 B slack)
+
+    ofdm::WalkArgs w{};
+    w.iq = reinterpret_cast<const double2*>(iq);
+    w.n = nn;
+    w.t2tw = c->d_t2tw;
+    const int sm = (int)c->p.smooth, f1 = (int)c->p.t2_sin_f1, f2 = (int)c->p.t2_sin_f2;
+    w.a1 = std::max(0, f1 - sm);
+    w.b1 = std::min(c->t2 - 1, f1 + sm);
+    w.a2 = std::max(0, f2 - sm);
+    w.b2 = std::min(c->t2 - 1, f2 + sm);
+    w.t2_level = (double)c->p.t2_sin_level / 1000;
+    w.templ = c->d_templ;
+    w.L = (int)c->p.pr_sin_len;
+    w.cycles = (int)(2 * c->p.t2sin_size + c->p.pr_sin_len);
+    w.pr_level = (double)c->p.pr_level / 1000;
+    w.pre = pre;
+    w.msg = msg;
+    w.chunk = chunk;
+    w.halo = halo;
+    w.max_rec = max_rec;
+    w.rec = d_rec;
+    w.nrec = d_nrec;
+    w.exit_pos = d_exit;
+    hipError_t e = ofdm::launch_stream_walk(c->t2_logn, w, nchunks, st);
+    if (e != hipSuccess) return hip_fail(e, "stream_walk launch");
+    std::vector<long> rec((size_t)nchunks * max_rec), ex(nchunks);
+    std::vector<int> nrec(nchunks);
+    HIP_TRY(hipMemcpyAsync(rec.data(), d_rec, rec_b, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(ex.data(), d_exit, nchunks * sizeof(long), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(nrec.data(), d_nrec, nchunks * sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+
+    // Stitch the chunk walks into the one true walk. Chunk 0 starts at the
+    // true initial state. Chunk k is accepted when its walk and the accepted
+    // walk before it locate a common frame no later than k's first owned
+    // frame (from there on both are the same computation); otherwise it is
+    // re-walked from the previous exit state (exact), with one workgroup.
+    auto rewalk = [&](long k, long start) -> int {
+        ofdm::WalkArgs r = w;
+        const int id = (int)k;
+        HIP_TRY(hipMemcpyAsync(d_start, &start, sizeof(long), hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(d_ids, &id, sizeof(int), hipMemcpyHostToDevice, st));
+        r.start_pos = d_start;
+        r.chunk_ids = d_ids;
+        hipError_t e2 = ofdm::launch_stream_walk(c->t2_logn, r, 1, st);
+        if (e2 != hipSuccess) return hip_fail(e2, "stream_walk re-walk launch");
+        HIP_TRY(hipMemcpyAsync(rec.data() + (size_t)k * max_rec, d_rec + (size_t)k * max_rec, max_rec * sizeof(long),
+                               hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(&ex[k], d_exit + k, sizeof(long), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(&nrec[k], d_nrec + k, sizeof(int), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        return OFDM_OK;
+    };
+    std::vector<long> frames;
+    std::vector<long> prev;  // every frame the accepted walk of the previous chunk located
+    long texit = 0;
+    for (long k = 0; k < nchunks; ++k) {
+        if (k > 0 && texit < 0) break;  // the true walk ended
+        if (nrec[k] > max_rec) return fail(OFDM_ERR_HIP, "stream walk record overflow");
+        std::vector<long> lst(rec.begin() + (size_t)k * max_rec, rec.begin() + (size_t)k * max_rec + nrec[k]);
+        const long lo = k * chunk, hi = lo + chunk;
+        if (k > 0) {
+            long first_owned = LONG_MAX;
+            for (long pb : lst)
+                if (pb >= lo && pb < hi) first_owned = std::min(first_owned, pb);
+            bool sync = false;
+            for (long pb : lst)
+                if (pb <= first_owned && std::find(prev.begin(), prev.end(), pb) != prev.end()) sync = true;
+            if (!sync) {
+                if ((rc = rewalk(k, texit))) return rc;
+                if (nrec[k] > max_rec) return fail(OFDM_ERR_HIP, "stream walk record overflow");
+                lst.assign(rec.begin() + (size_t)k * max_rec, rec.begin() + (size_t)k * max_rec + nrec[k]);
+            }
+        }
+        for (long pb : lst)
+            if (pb >= lo && pb < hi) frames.push_back(pb);
+        prev.swap(lst);
+        texit = ex[k];
+    }
+    *nframes_out = frames.size();
+    const size_t nout = std::min(frames.size(), max_frames);
+    if (nout == 0) return OFDM_OK;
+
+    // located frames -> batch -> main.cpp:60-80 chain + demod, in bounded batches
+    if ((rc = grow(c, c->s_pbs, nout * sizeof(long)))) return rc;
+    long* d_pbs = static_cast<long*>(c->s_pbs.p);
+    HIP_TRY(hipMemcpyAsync(d_pbs, frames.data(), nout * sizeof(long), hipMemcpyHostToDevice, st));
+    if (pb_out) HIP_TRY(hipMemcpyAsync(pb_out, d_pbs, nout * sizeof(long), hipMemcpyDeviceToDevice, st));
+    const size_t fb = (size_t)span * sizeof(double2);
+    const size_t bmax = std::max<size_t>(1, std::min<size_t>(65535, ((size_t)256 << 20) / fb));
+    const size_t nb0 = std::min(nout, bmax);
+    if ((rc = grow(c, c->s_batch, nb0 * fb)) || (rc = grow(c, c->s_chan, nb0 * c->D * sizeof(double2)))) return rc;
+    double* batch = static_cast<double*>(c->s_batch.p);
+    double* chan = static_cast<double*>(c->s_chan.p);
+    const long npts = (long)c->D * c->S;
+    for (size_t f0 = 0; f0 < nout; f0 += nb0) {
+        const size_t nb = std::min(nb0, nout - f0);
+        ofdm::GatherArgs ga{reinterpret_cast<const double2*>(iq), nn, d_pbs + f0, (long)nb, span,
+                            reinterpret_cast<double2*>(batch)};
+        e = ofdm::launch_gather(ga, st);
+        if (e != hipSuccess) return hip_fail(e, "gather launch");
+        if ((rc = ofdm_sync_frames(c, batch, nb, (size_t)span, OFDM_SYNC_ALL, nullptr, cfo_out ? cfo_out + f0 : nullptr,
+                                   chan, stream)))
+            return rc;
+        if ((rc = ofdm_rx_demod(c, batch + 2 * pre, nb, (size_t)span, chan, (size_t)c->D,
+                                constell_out ? constell_out + 2 * f0 * npts : nullptr,
+                                bytes_out ? bytes_out + f0 * c->geo.bytes_per_frame : nullptr, nullptr, nullptr,
+                                stream)))
+            return rc;
+    }
     return OFDM_OK;
 }
 

@@ -9,6 +9,9 @@
 //   cp_sync_kernel        OFDM_FORM::cp_freq_sinh         (Frame.hpp:238-263)
 //   phase_sync_kernel     OFDM_FORM::pr_phase_sinh        (Frame.hpp:265-274)
 //   chan_kernel           PREAMBLE_FORM::chan_char_lq     (Frame.hpp:389-434)
+//   stream_walk_kernel    the rx.cpp:125-221 detection walk, one walker per
+//                         stream chunk (find_t2sin + find_preamble per step)
+//   gather_kernel         copy located frames into a batch (rx.cpp:185-189)
 //
 // Arithmetic notes. The reference builds its phasor ramps by recursive
 // products (p *= step); here every sample's phasor is computed directly
@@ -600,6 +603,230 @@ hipError_t launch_chan(int logn, const ChanArgs& a, hipStream_t st)
         case 12: return chan_launch_n<12>(a, st);
         default: return hipErrorInvalidValue;
     }
+}
+
+// ========================================================================
+// Streaming detection walk (rx.cpp:125-221; oracle orc_stream_walk). One
+// 256-thread workgroup walks one chunk of the stream sequentially:
+//   hit = first T2 block with rel > level on the grid pos + k*T2sin_size
+//         (G blocks transformed per step, first hit taken);
+//   pb  = find_preamble(hit) + 1;  pb < -2 -> pos = hit + message;
+//   frame past the stream end -> stop;  else record pb, pos = pb + message.
+// A walker starts `halo` samples before its core [c*chunk, (c+1)*chunk) (or
+// at an exact state in a re-walk) and stops at the first state >= the core
+// end. The host accepts a chunk when its walk shares a located frame with
+// the previous chunk's (after which both walks are the same computation), and
+// re-walks it from the previous chunk's exit state otherwise.
+// ========================================================================
+namespace {
+
+constexpr int WALK_THREADS = 256;
+
+// PREAMBLE_FORM::find_preamble from s: first lag with norm > 1 and
+// |sum_j x[s+i+j] c_j| / sqrt(norm) > level (Frame.cpp:338-378), INT_MAX if
+// none. The running energy is the reference's serial recurrence (+ new, then
+// - old, separately rounded) on per-sample energies computed in parallel;
+// lags are tested 256 at a time with an early exit.
+__device__ int walk_preamble(const WalkArgs& a, long s, double2* xs, const double2* c, double* E, double* normv,
+                             int* best, int t)
+{
+    const int L = a.L, C = a.cycles;
+    for (int i = t; i < C + L; i += WALK_THREADS) {
+        const long j = s + i;
+        const double2 v = (j >= 0 && j < a.n) ? a.iq[j] : make_double2(0.0, 0.0);
+        xs[i] = v;
+        E[i] = __dadd_rn(__dmul_rn(v.x, v.x), __dmul_rn(v.y, v.y));
+    }
+    if (t == 0) *best = INT_MAX;
+    __syncthreads();
+    if (t == 0) {
+        double norm = 0.0;
+        for (int i = 0; i < L; ++i) norm = __dadd_rn(norm, E[i]);
+        for (int i = 0; i < C; ++i) {
+            normv[i] = norm;
+            norm = __dadd_rn(norm, E[i + L]);
+            norm = __dsub_rn(norm, E[i]);
+        }
+    }
+    __syncthreads();
+    int found = INT_MAX;
+    for (int base = 0; base < C; base += WALK_THREADS) {
+        const int i = base + t;
+        if (i < C) {
+            const double norm = normv[i];
+            if (norm > 1.0) {
+                double2 e = make_double2(0.0, 0.0);
+                for (int j = 0; j < L; ++j) e = cadd_rn(e, cmul_exact(xs[i + j], c[j]));
+                if (hypot(e.x, e.y) / sqrt(norm) > a.pr_level) atomicMin(best, i);
+            }
+        }
+        __syncthreads();
+        found = *best;
+        if (found != INT_MAX) break;  // uniform
+    }
+    __syncthreads();  // every thread has read *best before the next search resets it
+    return found;
+}
+
+}  // namespace
+
+template <int LOGT>
+__global__ void __launch_bounds__(WALK_THREADS) stream_walk_kernel(WalkArgs a)
+{
+    constexpr int N = 1 << LOGT, T = N / 8, G = WALK_THREADS / T;
+    static_assert(T <= WALK_THREADS, "T2sin_size <= 2048");
+    constexpr int NW = T >= 64 ? T / 64 : 1;  // waves per transform
+    extern __shared__ double2 smem[];
+    double2* lds_tw = smem;
+    double2* fftb = lds_tw + TwLds<LOGT>::SIZE;         // G * N
+    double2* red = fftb + G * N;                        // G * NW (tot, sine)
+    double2* ctap = red + G * NW;                       // L template taps
+    double2* xs = ctap + a.L;                           // cycles + L samples
+    double* E = reinterpret_cast<double*>(xs + a.cycles + a.L);  // cycles + L energies
+    double* normv = E + a.cycles + a.L;                 // cycles running energies
+    int* best = reinterpret_cast<int*>(normv + a.cycles);
+    int* bestg = best + 1;
+
+    const int t = threadIdx.x, g = t / T, tt = t - g * T;
+    const int c = a.chunk_ids ? a.chunk_ids[blockIdx.x] : (int)blockIdx.x;
+    load_twiddles<LOGT>(a.t2tw, lds_tw, t, WALK_THREADS);
+    for (int i = t; i < a.L; i += WALK_THREADS) ctap[i] = a.templ[i];
+    if (t == 0) *bestg = INT_MAX;
+    const long core0 = (long)c * a.chunk, end = core0 + a.chunk;
+    long pos = a.start_pos ? a.start_pos[blockIdx.x] : (c == 0 ? 0 : (core0 > a.halo ? core0 - a.halo : 0));
+    int nrec = 0;
+    long exitp = -1;
+    __syncthreads();
+    for (;;) {
+        if (pos >= end) {
+            exitp = pos;
+            break;
+        }
+        // find_t2sin(pos): blocks pos + k*N, G per step, first hit wins
+        long hit = -1;
+        bool stop = false;
+        for (long base = pos;; base += (long)G * N) {
+            if (base + N > a.n) {  // no full block left: the walk has consumed the stream
+                stop = true;
+                break;
+            }
+            if (base >= end) {  // scanning past the core: equivalent state, hand over
+                exitp = base;
+                stop = true;
+                break;
+            }
+            const long b = base + (long)g * N;
+            const bool live = b + N <= a.n;
+            double2 v[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = live ? a.iq[b + tt + T * i] : make_double2(0.0, 0.0);
+            fft_block<LOGT, -1>(v, tt, lds_tw, fftb + g * N);
+            double tot = 0.0, sine = 0.0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int k = tt + T * i;
+                const double2 z = fftb[g * N + lds_swz(k)];
+                const double e = z.x * z.x + z.y * z.y;
+                const double m = (double)((k >= a.a1 && k <= a.b1) + (k >= a.a2 && k <= a.b2));
+                tot += e;
+                sine += m * e;
+            }
+            constexpr int W0 = T >= 64 ? 32 : T / 2;
+#pragma unroll
+            for (int o = W0; o > 0; o >>= 1) {
+                tot += __shfl_xor(tot, o);
+                sine += __shfl_xor(sine, o);
+            }
+            if constexpr (NW > 1) {
+                if ((t & 63) == 0) red[g * NW + (tt >> 6)] = make_double2(tot, sine);
+                __syncthreads();
+                tot = 0.0;
+                sine = 0.0;
+                for (int w = 0; w < NW; ++w) {
+                    tot += red[g * NW + w].x;
+                    sine += red[g * NW + w].y;
+                }
+            }
+            if (tt == 0 && live && tot != 0.0) {
+                const double rel = sine / tot;
+                if (!isnan(rel) && rel > a.t2_level) atomicMin(bestg, g);
+            }
+            __syncthreads();
+            const int bg = *bestg;
+            __syncthreads();  // all have read bestg
+            if (t == 0) *bestg = INT_MAX;
+            if (bg != INT_MAX) {
+                hit = base + (long)bg * N;
+                break;
+            }
+        }
+        if (stop) break;
+        const int lag = walk_preamble(a, hit, xs, ctap, E, normv, best, t);
+        const long pb = (lag == INT_MAX ? -10 : hit + lag) + 1;  // rx.cpp:160
+        if (pb < -2) {                                            // rx.cpp:162-168
+            pos = hit + a.msg;
+            continue;
+        }
+        if (pb + a.pre + a.msg > a.n) break;  // frame not in the stream: the walk ends
+        if (t == 0 && nrec < a.max_rec) a.rec[(long)c * a.max_rec + nrec] = pb;
+        ++nrec;
+        pos = pb + a.msg;  // rx.cpp:192
+    }
+    if (t == 0) {
+        a.nrec[c] = nrec;
+        a.exit_pos[c] = exitp;
+    }
+}
+
+__global__ void gather_kernel(GatherArgs a)
+{
+    const long f = blockIdx.y;
+    const long s = a.starts[f];
+    double2* d = a.dst + f * a.span;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < a.span; i += (long)gridDim.x * blockDim.x) {
+        const long j = s + i;
+        d[i] = (j >= 0 && j < a.n) ? a.iq[j] : make_double2(0.0, 0.0);
+    }
+}
+
+template <int LOGT>
+static hipError_t walk_launch_n(const WalkArgs& a, long nblocks, hipStream_t st)
+{
+    constexpr int N = 1 << LOGT, T = N / 8, G = WALK_THREADS / T, NW = T >= 64 ? T / 64 : 1;
+    const size_t shm = sizeof(double2) * (TwLds<LOGT>::SIZE + (size_t)G * N + G * NW + a.L + a.cycles + a.L) +
+                       sizeof(double) * (2 * (size_t)a.cycles + a.L) + 16;
+    if (shm > 160 * 1024) return hipErrorInvalidValue;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)stream_walk_kernel<LOGT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL(stream_walk_kernel<LOGT>, dim3((unsigned)nblocks), dim3(WALK_THREADS), shm, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_stream_walk(int logt, const WalkArgs& a, long nblocks, hipStream_t st)
+{
+    if (nblocks <= 0) return hipSuccess;
+    switch (logt) {
+        case 6: return walk_launch_n<6>(a, nblocks, st);
+        case 7: return walk_launch_n<7>(a, nblocks, st);
+        case 8: return walk_launch_n<8>(a, nblocks, st);
+        case 9: return walk_launch_n<9>(a, nblocks, st);
+        case 10: return walk_launch_n<10>(a, nblocks, st);
+        case 11: return walk_launch_n<11>(a, nblocks, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_gather(const GatherArgs& a, hipStream_t st)
+{
+    if (a.nframes <= 0) return hipSuccess;
+    const long per = (a.span + 255) / 256;
+    const unsigned gx = (unsigned)(per < 64 ? per : 64);
+    hipLaunchKernelGGL(gather_kernel, dim3(gx, (unsigned)a.nframes), dim3(256), 0, st, a);
+    return hipGetLastError();
 }
 
 }  // namespace ofdm

@@ -71,6 +71,35 @@ struct ChanArgs {
     double pilot_ampl;
 };
 
+struct WalkArgs {
+    const double2* iq;          // stream
+    long n;
+    const double2* t2tw;        // T2sin_size forward twiddles
+    int a1, b1, a2, b2;         // T2 mask bands
+    double t2_level;
+    const double2* templ;       // pr_sin_len conj template
+    int L, cycles;              // pr_sin_len, 2*T2sin_size + pr_sin_len
+    double pr_level;
+    long pre, msg;              // preamble / message lengths (samples)
+    long chunk, halo;           // core samples per chunk; walk-in before the core
+    const int* chunk_ids;       // nullable: chunk of each workgroup (re-walk launches)
+    const long* start_pos;      // nullable: exact start state per workgroup (re-walk)
+    int max_rec;                // records per chunk
+    long* rec;                  // [chunk][max_rec] preamble starts found
+    int* nrec;                  // [chunk] frames found (> max_rec: overflow)
+    long* exit_pos;             // [chunk] walk state at exit; -1: stream exhausted
+};
+
+struct GatherArgs {
+    const double2* iq;
+    long n;
+    const long* starts;         // frame f copies [starts[f], starts[f] + span)
+    long nframes, span;
+    double2* dst;               // nframes * span
+};
+
+hipError_t launch_stream_walk(int logt, const WalkArgs& a, long nblocks, hipStream_t st);
+hipError_t launch_gather(const GatherArgs& a, hipStream_t st);
 hipError_t launch_t2_scan(int logn, const T2Args& a, int* first_out, hipStream_t st);
 hipError_t launch_find_preamble(const PreambleArgs& a, hipStream_t st);
 hipError_t launch_cfo(int logm, int g, const CfoArgs& a, hipStream_t st);

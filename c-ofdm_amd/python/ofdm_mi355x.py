@@ -98,6 +98,7 @@ SIGNATURES = {
     "ofdm_phase_sync": (_I, [_V, _V, _SZ, _SZ, _SZ, _V, _SZ, _V]),
     "ofdm_chan_estimate": (_I, [_V, _V, _SZ, _SZ, _V, _SZ, _V]),
     "ofdm_sync_frames": (_I, [_V, _V, _SZ, _SZ, _I, _V, _V, _V, _V]),
+    "ofdm_rx_stream": (_I, [_V, _V, _SZ, _SZ, _L, _V, _V, _V, _V, C.POINTER(_SZ), _V]),
 }
 
 _lib = None
@@ -280,6 +281,14 @@ class Modem:
         cs = self.params.num_data_subc if chan_stride is None else chan_stride
         check(lib().ofdm_chan_estimate(self.h, _ptr(x), nframes, frame_stride, _ptr(chan_out), cs,
                                        _stream(stream)))
+
+    def rx_stream(self, iq, n: int, max_frames: int, pb_out=None, bytes_out=None, constell_out=None,
+                  cfo_out=None, chunk: int = 0, stream=None) -> int:
+        """rx.cpp:125-221 over a device-resident stream; returns the frames found."""
+        m = C.c_size_t()
+        check(lib().ofdm_rx_stream(self.h, _ptr(iq), n, max_frames, chunk, _ptr(pb_out), _ptr(bytes_out),
+                                   _ptr(constell_out), _ptr(cfo_out), C.byref(m), _stream(stream)))
+        return m.value
 
     def sync_frames(self, frames, nframes: int, frame_stride: int, stages: int = SYNC_ALL,
                     cfo_in=None, cfo_out=None, chan_out=None, stream=None):

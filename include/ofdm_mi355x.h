@@ -266,6 +266,23 @@ int ofdm_sync_frames(ofdm_ctx* ctx, double* frames, size_t nframes, size_t frame
                      int stages, const double* cfo_in, double* cfo_out, double* chan_out,
                      void* stream);
 
+/* ---- streaming rx (rx.cpp:125-221) -------------------------------------
+ * Every frame the reference's detection walk finds in a contiguous stream of
+ * n complex samples (device), then the main.cpp:60-80 chain and demod on each:
+ *   pos = 0; hit = find_t2sin(pos); pb = find_preamble(hit) + 1;
+ *   pb < -2 -> pos = hit + message_len; frame past the end -> stop;
+ *   else the frame [pb, pb + preamble_len + message_len) is decoded and
+ *   pos = pb + message_len.
+ * The walk runs as parallel chunk walkers stitched into the one sequential
+ * walk (chunk = samples per walker, 0 = automatic). Outputs (device, nullable):
+ * pb_out[f] preamble start, bytes_out (bytes_per_frame per frame),
+ * constell_out (D*num_symb complex per frame), cfo_out. *nframes_out = frames
+ * found; outputs hold the first max_frames. The input is not modified.
+ * Synchronises `stream` (the host stitches the walk). */
+int ofdm_rx_stream(ofdm_ctx* ctx, const double* iq, size_t n, size_t max_frames, long chunk,
+                   long* pb_out, uint8_t* bytes_out, double* constell_out, double* cfo_out,
+                   size_t* nframes_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

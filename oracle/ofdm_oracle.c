@@ -789,3 +789,83 @@ void orc_tx_batch(const ofdm_params* p, const uint8_t* bytes, long nframes, doub
 #pragma omp parallel for num_threads(threads) schedule(static)
     for (long f = 0; f < nframes; f++) orc_ofdm_write(p, S, k, bytes + f * nb, iq + 2 * f * frame_stride);
 }
+
+
+/* ---- located-frame decode and the streaming walk (rx.cpp:125-221) ------ */
+
+/* main.cpp:60-80 / rx.cpp:181-216 on one located frame. `region` is
+ * [preamble | message] ((N+cp)*(npr+S) samples); it is copied first, as
+ * rx.cpp:185-189 copies it into FRAME_FORM::buf. Writes D*S equalised points
+ * (before demod's clamp, data/constell.bin layout) and D*S*k/8 bytes; returns
+ * the pilot_freq_sinh CFO. */
+double orc_decode_frame(const ofdm_params* p, const double* region, double* constell, uint8_t* bytes)
+{
+    int N = (int)p->fft_size, cp = (int)p->cp_size, L = N + cp;
+    int npr = (int)p->num_pr_symb, S = (int)p->num_symb, D = (int)p->num_data_subc;
+    int k = (int)p->mod_type;
+    long pre = (long)L * npr, msg = (long)L * S;
+    cplx* x = (cplx*)malloc(sizeof(cplx) * (pre + msg));
+    memcpy(x, region, sizeof(cplx) * (pre + msg));
+    cplx* opre = (cplx*)malloc(sizeof(cplx) * pre);
+    cplx* modp = (cplx*)malloc(sizeof(cplx) * (long)D * npr);
+    cplx* templ = (cplx*)malloc(sizeof(cplx) * p->pr_sin_len);
+    cplx* chan = (cplx*)malloc(sizeof(cplx) * D);
+    orc_preamble_setup(p, (double*)opre, (double*)modp, (double*)templ);
+    double cfo = orc_pilot_freq_sinh(p, npr, (const double*)x);          /* main.cpp:60 */
+    orc_freq_shift((double*)x, pre + msg, cfo);                          /* main.cpp:61 */
+    orc_cp_freq_sinh(p, npr + S, (double*)x);                            /* main.cpp:62 */
+    orc_pr_phase_sinh((double*)x, pre + msg, (const double*)opre, pre);  /* main.cpp:63 */
+    orc_chan_char_lq(p, (double*)x, (const double*)modp, (double*)chan); /* main.cpp:65 */
+    cplx* c = (cplx*)constell;
+    orc_ofdm_fft(p, S, (const double*)(x + pre), constell);              /* main.cpp:66 */
+    long npts = (long)D * S;
+    for (long j = 0; j < npts; j++) c[j] /= chan[j % D];                 /* main.cpp:69-71 */
+    cplx* tmp = (cplx*)malloc(sizeof(cplx) * npts);
+    memcpy(tmp, c, sizeof(cplx) * npts);
+    orc_demod(k, (double*)tmp, (size_t)npts, bytes);                     /* main.cpp:73 (clamps its copy) */
+    free(tmp);
+    free(chan);
+    free(templ);
+    free(modp);
+    free(opre);
+    free(x);
+    return cfo;
+}
+
+/* The detection walk of rx.cpp:125-221 over one contiguous stream (the
+ * ring-buffer refills of rx.cpp keep absolute positions, so over a stream
+ * held whole they are the identity):
+ *   pos = 0; loop { hit = find_t2sin(pos) (256-sample grid from pos);
+ *   none -> stop; pb = find_preamble(hit) + 1 (rx.cpp:160);
+ *   pb < -2 -> pos = hit + message.size (rx.cpp:162-168);
+ *   frame [pb, pb + preamble + message) past the stream end -> stop;
+ *   record pb; pos = pb + message.size (rx.cpp:192) }.
+ * Samples past n read as zero in the preamble search. Returns the number of
+ * frames (at most max) and their preamble starts. */
+long orc_stream_walk(const ofdm_params* p, const double* x, long n, long* pb_out, long max)
+{
+    int N = (int)p->fft_size, cp = (int)p->cp_size, L = N + cp;
+    long pre = (long)L * p->num_pr_symb, msg = (long)L * p->num_symb;
+    int D = (int)p->num_data_subc;
+    cplx* opre = (cplx*)malloc(sizeof(cplx) * pre);
+    cplx* modp = (cplx*)malloc(sizeof(cplx) * (long)D * p->num_pr_symb);
+    cplx* templ = (cplx*)malloc(sizeof(cplx) * p->pr_sin_len);
+    orc_preamble_setup(p, (double*)opre, (double*)modp, (double*)templ);
+    long pos = 0, nf = 0;
+    while (nf < max) {
+        long hit = orc_find_t2sin(p, x, n, pos);
+        if (hit < 0) break;
+        long pb = orc_find_preamble(p, (const double*)templ, x, n, hit) + 1;
+        if (pb < -2) {
+            pos = hit + msg;
+            continue;
+        }
+        if (pb + pre + msg > n) break;
+        pb_out[nf++] = pb;
+        pos = pb + msg;
+    }
+    free(templ);
+    free(modp);
+    free(opre);
+    return nf;
+}

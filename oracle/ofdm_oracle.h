@@ -83,6 +83,11 @@ unsigned long long orc_rx_batch(const ofdm_params* p, const double* iq, long nfr
 void orc_tx_batch(const ofdm_params* p, const uint8_t* bytes, long nframes, double* iq,
                   long frame_stride, int threads);
 
+/* Located-frame decode (main.cpp:60-80) and the streaming detection walk
+ * (rx.cpp:125-221) over a contiguous stream. */
+double orc_decode_frame(const ofdm_params* p, const double* region, double* constell, uint8_t* bytes);
+long orc_stream_walk(const ofdm_params* p, const double* x, long n, long* pb_out, long max);
+
 #ifdef __cplusplus
 }
 #endif

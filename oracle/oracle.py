@@ -100,6 +100,8 @@ def lib():
             "orc_awgn": (v, [P_d, l, d, u64, u64]),
             "orc_rx_batch": (u64, [PP, P_d, l, l, P_d, P_u8, P_u8, i]),
             "orc_tx_batch": (v, [PP, P_u8, l, P_d, l, i]),
+            "orc_decode_frame": (d, [PP, P_d, P_d, P_u8]),
+            "orc_stream_walk": (l, [PP, P_d, l, C.POINTER(C.c_long), l]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -360,3 +362,24 @@ def tx_batch(params, data: np.ndarray, nframes: int, frame_stride: int | None = 
     assert len(data) >= nframes * g["bytes_per_frame"]
     lib().orc_tx_batch(C.byref(p), _u8(data), nframes, _d(out), stride, threads)
     return out
+
+
+def decode_frame(params, region: np.ndarray):
+    """main.cpp:60-80 on one [preamble | message] region -> (cfo, constell, bytes)."""
+    p = P(params)
+    g = geometry(p)
+    region = np.ascontiguousarray(region, np.complex128)
+    assert len(region) >= g["preamble_len"] + g["message_len"]
+    cons = np.zeros(g["npts"], np.complex128)
+    out = np.zeros(g["bytes_per_frame"], np.uint8)
+    cfo = lib().orc_decode_frame(C.byref(p), _d(region), _d(cons), _u8(out))
+    return cfo, cons, out
+
+
+def stream_walk(params, x: np.ndarray, max_frames: int = 1 << 20) -> np.ndarray:
+    """rx.cpp:125-221 detection walk over a contiguous stream -> preamble starts."""
+    p = P(params)
+    x = np.ascontiguousarray(x, np.complex128)
+    out = np.zeros(max_frames, np.int64)
+    nf = lib().orc_stream_walk(C.byref(p), _d(x), len(x), out.ctypes.data_as(C.POINTER(C.c_long)), max_frames)
+    return out[:nf].copy()

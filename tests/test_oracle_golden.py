@@ -75,3 +75,22 @@ def test_fft_is_the_dft_definition():
         x = rng.standard_normal(n) + 1j * rng.standard_normal(n)
         assert rel_err(O.fft(x, -1), np.fft.fft(x)) < 1e-13
         assert rel_err(O.fft(x, +1), np.fft.ifft(x) * n) < 1e-13
+
+
+def test_stream_walk_and_decode_match_reference_capture():
+    """The rx.cpp:125-221 walk over data/data.bin finds both frames at the
+    reference's preamble starts; the located-frame decode (main.cpp:60-80)
+    reproduces cfo, constell.bin and data.txt."""
+    pbs = O.stream_walk(G, GD["data"])
+    assert list(pbs) == list(GD["preamble_begin"])
+    g = O.geometry(G)
+    span = g["preamble_len"] + g["message_len"]
+    cfo, cons, out = O.decode_frame(G, GD["data"][pbs[0]: pbs[0] + span])
+    assert cfo == GD["cfo_frame1"]
+    assert rel_err(cons, GD["constell"]) < 1e-12
+    assert np.array_equal(out, GD["payload"])
+    _, _, out2 = O.decode_frame(G, GD["data"][pbs[1]: pbs[1] + span])
+    assert np.array_equal(out2, GD["payload"])
+    # a stream cut inside frame 2 yields frame 1 only; before frame 1's end, none
+    assert list(O.stream_walk(G, GD["data"][: pbs[1] + span - 1])) == [pbs[0]]
+    assert list(O.stream_walk(G, GD["data"][: pbs[0] + span - 1])) == []
