@@ -73,29 +73,50 @@ def payload_bytes(begin: int, count: int, seed: int = 0x5EED) -> np.ndarray:
     return (z & np.uint64(0xFF)).astype(np.uint8)
 
 
-def cpu_baseline(p, data_host: np.ndarray, nframes_sample: int, noise_std: float, budget_s: float):
-    """Oracle (plain-C restatement) tx+AWGN+rx loopback on host cores, 1 thread,
-    on a bounded sample of the same workload. Reported beside the GPU number."""
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown CPU"
+
+
+def cpu_baseline(p, data_host: np.ndarray, noise_std: float, budget_s: float, threads: int):
+    """Oracle (plain-C restatement) tx+AWGN+rx loopback on host cores over a
+    bounded sample of the same workload: single-threaded (one frame at a time,
+    as the reference runs) and OpenMP over `threads` cores (one frame per
+    thread). Reported beside the GPU number; `value` is the all-cores rate."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     g = O.geometry(p)
-    bpf = g["bytes_per_frame"]
-    done = 0
-    t0 = time.perf_counter()
-    while True:
-        for f in range(nframes_sample):
-            iq = O.tx_batch(p, data_host[f * bpf:(f + 1) * bpf], 1)
-            iq = O.awgn(iq, noise_std, seed=1, sample_offset=f * g["message_len"])
-            O.rx_batch(p, iq, 1, g["message_len"], ref=data_host[f * bpf:(f + 1) * bpf],
-                       want_constell=True)
-        done += nframes_sample
-        el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
-    samples = done * g["message_len"]
-    return {"value": samples / el, "unit": "IQ-samples/s", "cores": 1, "kind": "port",
-            "sample": f"{done} frames of the same config-B workload (oracle/ofdm_oracle.c tx+AWGN+rx "
-                      f"loopback, 1 thread, own radix-4/2 FFT; FFTW absent), {el:.1f} s"}
+    bpf, msg = g["bytes_per_frame"], g["message_len"]
+    nf_avail = len(data_host) // bpf
+
+    def run(nthreads, batch, budget):
+        done, f0 = 0, 0
+        t0 = time.perf_counter()
+        while True:
+            nb = min(batch, nf_avail - f0)
+            d = data_host[f0 * bpf:(f0 + nb) * bpf]
+            iq = O.tx_batch(p, d, nb, threads=nthreads)
+            iq = O.awgn(iq, noise_std, seed=1, sample_offset=f0 * msg, threads=nthreads)
+            O.rx_batch(p, iq, nb, msg, ref=d, threads=nthreads, want_constell=True)
+            done += nb
+            f0 = (f0 + nb) % max(1, nf_avail - batch)
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return done * msg / el, done, el
+
+    st, st_frames, st_s = run(1, 4, budget_s / 2)
+    mt, mt_frames, mt_s = run(threads, 4 * threads, budget_s / 2)
+    return {"value": mt, "unit": "IQ-samples/s", "cores": threads, "kind": "port",
+            "single_thread_value": st,
+            "sample": (f"config-B tx+AWGN+rx loopback (oracle/ofdm_oracle.c, own radix-4/2 FFT; FFTW absent) "
+                       f"on {_cpu_model()} (os.cpu_count()={os.cpu_count()}): {mt_frames} frames on {threads} "
+                       f"OpenMP threads in {mt_s:.1f} s; {st_frames} frames single-threaded in {st_s:.1f} s")}
 
 
 def main():
@@ -107,7 +128,8 @@ def main():
     ap.add_argument("--total-frames", type=int, default=0,
                     help="strong scaling: shard this many frames over the GPUs (config 5: 30517 = 10 GB)")
     ap.add_argument("--snr-db", type=float, default=10.0)
-    ap.add_argument("--cpu-budget", type=float, default=8.0)
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline (half 1 thread, half all)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: min(16, cpu_count))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -240,7 +262,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            result["cpu_baseline"] = cpu_baseline(p, data_host, 4, noise_std, args.cpu_budget)
+            thr = args.cpu_threads or min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16
+            result["cpu_baseline"] = cpu_baseline(p, data_host, noise_std, args.cpu_budget, thr)
         except Exception as e:  # reported, not fatal: the GPU number stands alone
             result["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:

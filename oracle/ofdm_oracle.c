@@ -738,10 +738,20 @@ static inline uint32_t lowbias32(uint32_t x)
 void orc_awgn(double* xd, long n, double noise_std, unsigned long long seed,
               unsigned long long off)
 {
+    orc_awgn_mt(xd, n, noise_std, seed, off, 1);
+}
+
+/* orc_awgn on `threads` OpenMP threads (the noise is counter-based, so the
+ * result does not depend on the thread count). */
+void orc_awgn_mt(double* xd, long n, double noise_std, unsigned long long seed,
+                 unsigned long long off, int threads)
+{
     cplx* x = (cplx*)xd;
     double sc = noise_std * M_SQRT1_2;
     const uint32_t k0 = lowbias32((uint32_t)seed ^ 0x9E3779B9u);
     const uint32_t k1 = lowbias32((uint32_t)(seed >> 32) + k0);
+    if (threads < 1) threads = 1;
+#pragma omp parallel for num_threads(threads) schedule(static)
     for (long i = 0; i < n; i++) {
         uint64_t g = off + (uint64_t)i;
         uint32_t h1 = lowbias32((uint32_t)g ^ lowbias32((uint32_t)(g >> 32) ^ k1) ^ k0);

@@ -74,6 +74,8 @@ void orc_get_int16(const double* x, long n, long mult, int16_t* out);
 /* Loopback channel used by the bench (not in the reference): counter-based AWGN. */
 void orc_awgn(double* x, long n, double noise_std, unsigned long long seed,
               unsigned long long sample_offset);
+void orc_awgn_mt(double* x, long n, double noise_std, unsigned long long seed,
+                 unsigned long long sample_offset, int threads);
 
 /* Batched rx over message frames, optionally OpenMP-parallel over frames
  * (cpu_baseline leg). Returns bit errors vs ref (if ref != NULL). */

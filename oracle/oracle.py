@@ -98,6 +98,7 @@ def lib():
             "orc_frame_write": (v, [PP, P_u8, P_d]),
             "orc_get_int16": (v, [P_d, l, l, P_i16]),
             "orc_awgn": (v, [P_d, l, d, u64, u64]),
+            "orc_awgn_mt": (v, [P_d, l, d, u64, u64, i]),
             "orc_rx_batch": (u64, [PP, P_d, l, l, P_d, P_u8, P_u8, i]),
             "orc_tx_batch": (v, [PP, P_u8, l, P_d, l, i]),
             "orc_decode_frame": (d, [PP, P_d, P_d, P_u8]),
@@ -333,9 +334,9 @@ def get_int16(x: np.ndarray, mult: int) -> np.ndarray:
     return out
 
 
-def awgn(x: np.ndarray, noise_std: float, seed: int, sample_offset: int = 0) -> np.ndarray:
+def awgn(x: np.ndarray, noise_std: float, seed: int, sample_offset: int = 0, threads: int = 1) -> np.ndarray:
     x = np.array(x, np.complex128, copy=True)
-    lib().orc_awgn(_d(x), len(x), noise_std, seed, sample_offset)
+    lib().orc_awgn_mt(_d(x), len(x), noise_std, seed, sample_offset, threads)
     return x
 
 

@@ -94,3 +94,14 @@ def test_stream_walk_and_decode_match_reference_capture():
     # a stream cut inside frame 2 yields frame 1 only; before frame 1's end, none
     assert list(O.stream_walk(G, GD["data"][: pbs[1] + span - 1])) == [pbs[0]]
     assert list(O.stream_walk(G, GD["data"][: pbs[0] + span - 1])) == []
+
+
+def test_awgn_is_counter_based_and_thread_independent():
+    x = np.zeros(100003, np.complex128)
+    a = O.awgn(x, 0.5, seed=17, sample_offset=(1 << 32) - 50000)
+    b = O.awgn(x, 0.5, seed=17, sample_offset=(1 << 32) - 50000, threads=4)
+    assert np.array_equal(a, b)
+    # a sub-range at its global offset is the same noise
+    c = O.awgn(x[:1000], 0.5, seed=17, sample_offset=(1 << 32) - 50000 + 777)
+    assert np.array_equal(c, a[777:1777])
+    assert abs(np.mean(np.abs(a) ** 2) - 0.25) < 0.01
