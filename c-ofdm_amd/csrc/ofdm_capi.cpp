@@ -698,13 +698,17 @@ int ofdm_tx_frames(ofdm_ctx* c, const uint8_t* bytes, size_t nframes, double* fr
     return OFDM_OK;
 }
 
-int ofdm_rx_demod(ofdm_ctx* c, const double* iq, size_t nframes, size_t frame_stride, const double* chan,
-                  size_t chan_stride, double* constell_out, uint8_t* bytes_out, const uint8_t* ref_bytes,
-                  unsigned long long* bit_errors, void* stream)
+}  // extern "C"
+
+// ofdm_rx_demod / ofdm_rx_demod_i16: exactly one of iq, iq16 is set.
+static int rx_demod_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, size_t nframes, size_t frame_stride,
+                         const double* chan, size_t chan_stride, double* constell_out, uint8_t* bytes_out,
+                         const uint8_t* ref_bytes, unsigned long long* bit_errors, void* stream)
 {
-    if (!c || !iq) return fail(OFDM_ERR_INVALID, "null argument");
+    if (!c || (!iq && !iq16)) return fail(OFDM_ERR_INVALID, "null argument");
+    if (iq16 && ((uintptr_t)iq16 & 3)) return fail(OFDM_ERR_INVALID, "iq16 must be 4-byte aligned");
     if (frame_stride < (size_t)c->geo.message_len) return fail(OFDM_ERR_INVALID, "frame_stride < message_len");
-    if (!aligned16(iq) || (chan && !aligned16(chan)) || (constell_out && !aligned16(constell_out)))
+    if ((iq && !aligned16(iq)) || (chan && !aligned16(chan)) || (constell_out && !aligned16(constell_out)))
         return fail(OFDM_ERR_INVALID, "complex buffers must be 16-byte aligned");
     if ((ref_bytes == nullptr) != (bit_errors == nullptr))
         return fail(OFDM_ERR_INVALID, "ref_bytes and bit_errors go together");
@@ -712,7 +716,8 @@ int ofdm_rx_demod(ofdm_ctx* c, const double* iq, size_t nframes, size_t frame_st
     if (nframes > 0x7fffffffu) return fail(OFDM_ERR_INVALID, "too many frames in one call");
     ofdm::RxArgs a{};
     a.tab = c->tables(false);
-    a.iq = reinterpret_cast<const double2*>(iq);
+    a.iq = iq16 ? nullptr : reinterpret_cast<const double2*>(iq);
+    a.iq16 = reinterpret_cast<const short2*>(iq16);
     a.nframes = (long)nframes;
     a.frame_stride = (long)frame_stride;
     a.chan = reinterpret_cast<const double2*>(chan);
@@ -751,6 +756,26 @@ int ofdm_rx_demod(ofdm_ctx* c, const double* iq, size_t nframes, size_t frame_st
     hipError_t e = ofdm::launch_rx(c->logn, a, (hipStream_t)stream, nullptr);
     if (e != hipSuccess) return hip_fail(e, "rx_kernel launch");
     return OFDM_OK;
+}
+
+extern "C" {
+
+int ofdm_rx_demod(ofdm_ctx* c, const double* iq, size_t nframes, size_t frame_stride, const double* chan,
+                  size_t chan_stride, double* constell_out, uint8_t* bytes_out, const uint8_t* ref_bytes,
+                  unsigned long long* bit_errors, void* stream)
+{
+    if (!iq) return fail(OFDM_ERR_INVALID, "null argument");
+    return rx_demod_impl(c, iq, nullptr, nframes, frame_stride, chan, chan_stride, constell_out, bytes_out, ref_bytes,
+                         bit_errors, stream);
+}
+
+int ofdm_rx_demod_i16(ofdm_ctx* c, const int16_t* iq16, size_t nframes, size_t frame_stride, const double* chan,
+                      size_t chan_stride, double* constell_out, uint8_t* bytes_out, const uint8_t* ref_bytes,
+                      unsigned long long* bit_errors, void* stream)
+{
+    if (!iq16) return fail(OFDM_ERR_INVALID, "null argument");
+    return rx_demod_impl(c, nullptr, iq16, nframes, frame_stride, chan, chan_stride, constell_out, bytes_out,
+                         ref_bytes, bit_errors, stream);
 }
 
 int ofdm_demap(ofdm_ctx* c, double* points, size_t n, uint8_t* bytes_out, void* stream)
@@ -1038,14 +1063,18 @@ int ofdm_sync_frames(ofdm_ctx* c, double* frames, size_t nframes, size_t stride,
     return OFDM_OK;
 }
 
-int ofdm_rx_stream(ofdm_ctx* c, const double* iq, size_t n, size_t max_frames, long chunk, long* pb_out,
-                   uint8_t* bytes_out, double* constell_out, double* cfo_out, size_t* nframes_out, void* stream)
+}  // extern "C"
+
+// ofdm_rx_stream / ofdm_rx_stream_i16: exactly one of iq, iq16 is set.
+static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, size_t n, size_t max_frames,
+                          long chunk, long* pb_out, uint8_t* bytes_out, double* constell_out, double* cfo_out,
+                          size_t* nframes_out, void* stream)
 {
-    if (!c || !iq || !nframes_out) return fail(OFDM_ERR_INVALID, "null argument");
+    if (!c || (!iq && !iq16) || !nframes_out) return fail(OFDM_ERR_INVALID, "null argument");
     *nframes_out = 0;
     if (c->t2_logn < 6 || c->t2_logn > 11) return fail(OFDM_ERR_UNSUPPORTED, "stream walk needs T2sin_size = 2^a, 64..2048");
-    if (!aligned16(iq) || (constell_out && !aligned16(constell_out)))
-        return fail(OFDM_ERR_INVALID, "complex buffers must be 16-byte aligned");
+    if ((iq && !aligned16(iq)) || (iq16 && ((uintptr_t)iq16 & 3)) || (constell_out && !aligned16(constell_out)))
+        return fail(OFDM_ERR_INVALID, "misaligned buffer (complex<double> 16 B, complex<int16> 4 B)");
     if (n > (size_t)1 << 40) return fail(OFDM_ERR_INVALID, "stream too long");
     hipStream_t st = (hipStream_t)stream;
     const long L = c->L, pre = (long)L * c->npr, msg = (long)L * c->S, span = pre + msg;
@@ -1074,6 +1103,7 @@ int ofdm_rx_stream(ofdm_ctx* c, const double* iq, size_t n, size_t max_frames, l
 
     ofdm::WalkArgs w{};
     w.iq = reinterpret_cast<const double2*>(iq);
+    w.iq16 = reinterpret_cast<const short2*>(iq16);
     w.n = nn;
     w.t2tw = c->d_t2tw;
     const int sm = (int)c->p.smooth, f1 = (int)c->p.t2_sin_f1, f2 = (int)c->p.t2_sin_f2;
@@ -1168,8 +1198,8 @@ int ofdm_rx_stream(ofdm_ctx* c, const double* iq, size_t n, size_t max_frames, l
     const long npts = (long)c->D * c->S;
     for (size_t f0 = 0; f0 < nout; f0 += nb0) {
         const size_t nb = std::min(nb0, nout - f0);
-        ofdm::GatherArgs ga{reinterpret_cast<const double2*>(iq), nn, d_pbs + f0, (long)nb, span,
-                            reinterpret_cast<double2*>(batch)};
+        ofdm::GatherArgs ga{reinterpret_cast<const double2*>(iq), reinterpret_cast<const short2*>(iq16), nn,
+                            d_pbs + f0, (long)nb, span, reinterpret_cast<double2*>(batch)};
         e = ofdm::launch_gather(ga, st);
         if (e != hipSuccess) return hip_fail(e, "gather launch");
         if ((rc = ofdm_sync_frames(c, batch, nb, (size_t)span, OFDM_SYNC_ALL, nullptr, cfo_out ? cfo_out + f0 : nullptr,
@@ -1182,6 +1212,24 @@ int ofdm_rx_stream(ofdm_ctx* c, const double* iq, size_t n, size_t max_frames, l
             return rc;
     }
     return OFDM_OK;
+}
+
+extern "C" {
+
+int ofdm_rx_stream(ofdm_ctx* c, const double* iq, size_t n, size_t max_frames, long chunk, long* pb_out,
+                   uint8_t* bytes_out, double* constell_out, double* cfo_out, size_t* nframes_out, void* stream)
+{
+    if (!iq) return fail(OFDM_ERR_INVALID, "null argument");
+    return rx_stream_impl(c, iq, nullptr, n, max_frames, chunk, pb_out, bytes_out, constell_out, cfo_out,
+                          nframes_out, stream);
+}
+
+int ofdm_rx_stream_i16(ofdm_ctx* c, const int16_t* iq16, size_t n, size_t max_frames, long chunk, long* pb_out,
+                       uint8_t* bytes_out, double* constell_out, double* cfo_out, size_t* nframes_out, void* stream)
+{
+    if (!iq16) return fail(OFDM_ERR_INVALID, "null argument");
+    return rx_stream_impl(c, nullptr, iq16, n, max_frames, chunk, pb_out, bytes_out, constell_out, cfo_out,
+                          nframes_out, stream);
 }
 
 }  // extern "C"

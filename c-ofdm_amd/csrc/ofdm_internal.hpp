@@ -43,6 +43,7 @@ struct TxArgs {
 struct RxArgs {
     DevTables tab;
     const double2* iq;          // frame f message at iq + f*frame_stride
+    const short2* iq16;         // or: complex<int16> input, same indexing (FRAME_FORM::form_int16_to_double fused)
     long nframes;
     long frame_stride;
     const double2* chan;        // nullable: D divisors per frame

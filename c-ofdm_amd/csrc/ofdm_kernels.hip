@@ -306,15 +306,42 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) tx_kernel(TxArgs a)
 //   (S <= RX_SMAX, D <= RX_DPT*T), written through a wave-uniform switch on
 //   the symbol index so every register index is compile-time.
 // STAGED=true: any S; inputs parked in a.ystage (same-thread re-read).
-template <int LOGN>
-__device__ __forceinline__ void load_symbol(double2 (&r)[8], const double2* __restrict__ src, int t)
-{
-    constexpr int T = (1 << LOGN) / 8;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) r[i] = load_nt(src + t + T * i);
-}
+// The next symbol's 8 samples per thread, held in registers across the FFT:
+// complex<double> (4 VGPRs each) or, for wire-format input, complex<int16>
+// (1 VGPR each, converted exactly on use: FRAME_FORM::form_int16_to_double,
+// Frame.hpp:472-481, fused).
+template <int LOGN, bool I16>
+struct SymbolRegs;
 
-template <int LOGN, bool STAGED>
+template <int LOGN>
+struct SymbolRegs<LOGN, false> {
+    double2 r[8];
+    __device__ __forceinline__ void load(const RxArgs& a, long off, int t)
+    {
+        constexpr int T = (1 << LOGN) / 8;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r[i] = load_nt(a.iq + off + t + T * i);
+    }
+    __device__ __forceinline__ double2 get(int i) const { return r[i]; }
+};
+
+template <int LOGN>
+struct SymbolRegs<LOGN, true> {
+    int r[8];
+    __device__ __forceinline__ void load(const RxArgs& a, long off, int t)
+    {
+        constexpr int T = (1 << LOGN) / 8;
+        const int* p = reinterpret_cast<const int*>(a.iq16 + off);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r[i] = __builtin_nontemporal_load(p + t + T * i);
+    }
+    __device__ __forceinline__ double2 get(int i) const
+    {
+        return make_double2((double)(int)(short)(r[i] & 0xffff), (double)(r[i] >> 16));
+    }
+};
+
+template <int LOGN, bool STAGED, bool I16>
 __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
 {
     using FS = FftShape<LOGN>;
@@ -333,7 +360,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
     const int t = threadIdx.x;
     const long f = blockIdx.x;
     const int L = N + a.cp;
-    const double2* x = a.iq + f * a.frame_stride + a.cp;  // CP strip (Frame.hpp:278-279)
+    const long x0 = f * a.frame_stride + a.cp;  // CP strip (Frame.hpp:278-279)
 
     // table loads first, then symbol 0: every prologue wait below is a
     // counted vmcnt that leaves the symbol prefetch in flight
@@ -349,8 +376,8 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
 #pragma unroll
     for (int i = 0; i < RX_DPT; ++i) pk[i] = a.tab.rx_pack[t + T * i];
     const int pbin = a.tab.pilot_swz[t];
-    double2 pf[8];
-    load_symbol<LOGN>(pf, x, t);
+    SymbolRegs<LOGN, I16> pf;
+    pf.load(a, x0, t);
     if constexpr (kTwSplit) tw_store<LOGN>(twp, lds_tw);  // read after pass 0's barrier
 
     double2 y[SW][RX_DPT];
@@ -360,8 +387,8 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
     for (int s = 0; s < S; ++s) {
         double2 v[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = pf[i];
-        if (s + 1 < S) load_symbol<LOGN>(pf, x + (long)(s + 1) * L, t);
+        for (int i = 0; i < 8; ++i) v[i] = pf.get(i);
+        if (s + 1 < S) pf.load(a, x0 + (long)(s + 1) * L, t);
         // opaque copy of t: the per-pass LDS addresses are recomputed each
         // symbol instead of being hoisted out of the loop and held live
         // beside the register window
@@ -600,7 +627,7 @@ static size_t rx_shm(const RxArgs& a)
     return sizeof(double2) * (FS::N + FS::PADN + TwLds<LOGN>::SIZE + 2 * (size_t)a.S * a.P) + 32 * sizeof(double);
 }
 
-template <int LOGN, bool STAGED>
+template <int LOGN, bool STAGED, bool I16>
 static hipError_t rx_launch_n(const RxArgs& a, hipStream_t st)
 {
     using FS = FftShape<LOGN>;
@@ -608,12 +635,12 @@ static hipError_t rx_launch_n(const RxArgs& a, hipStream_t st)
     if (shm > 160 * 1024) return hipErrorInvalidValue;
     static int attr = 0;
     if ((size_t)attr < shm) {
-        (void)hipFuncSetAttribute((const void*)rx_kernel<LOGN, STAGED>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)rx_kernel<LOGN, STAGED, I16>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             160 * 1024);
         attr = 160 * 1024;
     }
     if (a.nframes <= 0) return hipSuccess;
-    hipLaunchKernelGGL((rx_kernel<LOGN, STAGED>), dim3((unsigned)a.nframes), dim3(FS::T), shm, st, a);
+    hipLaunchKernelGGL((rx_kernel<LOGN, STAGED, I16>), dim3((unsigned)a.nframes), dim3(FS::T), shm, st, a);
     return hipGetLastError();
 }
 
@@ -625,7 +652,8 @@ static hipError_t rx_dispatch(const RxArgs& a, hipStream_t st, bool* staged)
     if (staged) *staged = !fits;
     if (a.P > FS::T) return hipErrorInvalidValue;
     if (!fits && a.ystage == nullptr) return hipErrorInvalidValue;
-    return fits ? rx_launch_n<LOGN, false>(a, st) : rx_launch_n<LOGN, true>(a, st);
+    if (a.iq16) return fits ? rx_launch_n<LOGN, false, true>(a, st) : rx_launch_n<LOGN, true, true>(a, st);
+    return fits ? rx_launch_n<LOGN, false, false>(a, st) : rx_launch_n<LOGN, true, false>(a, st);
 }
 
 hipError_t launch_rx(int logn, const RxArgs& a, hipStream_t st, bool* staged)

@@ -622,6 +622,19 @@ namespace {
 
 constexpr int WALK_THREADS = 256;
 
+// Stream sample j as complex<double> (int16 wire samples convert exactly, as
+// FRAME_FORM::form_int16_to_double, Frame.hpp:472-481); zero outside [0, n).
+template <class A>
+__device__ __forceinline__ double2 stream_sample(const A& a, long j)
+{
+    if (j < 0 || j >= a.n) return make_double2(0.0, 0.0);
+    if (a.iq16) {
+        const short2 v = a.iq16[j];
+        return make_double2((double)v.x, (double)v.y);
+    }
+    return a.iq[j];
+}
+
 // PREAMBLE_FORM::find_preamble from s: first lag with norm > 1 and
 // |sum_j x[s+i+j] c_j| / sqrt(norm) > level (Frame.cpp:338-378), INT_MAX if
 // none. The running energy is the reference's serial recurrence (+ new, then
@@ -632,8 +645,7 @@ __device__ int walk_preamble(const WalkArgs& a, long s, double2* xs, const doubl
 {
     const int L = a.L, C = a.cycles;
     for (int i = t; i < C + L; i += WALK_THREADS) {
-        const long j = s + i;
-        const double2 v = (j >= 0 && j < a.n) ? a.iq[j] : make_double2(0.0, 0.0);
+        const double2 v = stream_sample(a, s + i);
         xs[i] = v;
         E[i] = __dadd_rn(__dmul_rn(v.x, v.x), __dmul_rn(v.y, v.y));
     }
@@ -719,7 +731,7 @@ __global__ void __launch_bounds__(WALK_THREADS) stream_walk_kernel(WalkArgs a)
             const bool live = b + N <= a.n;
             double2 v[8];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) v[i] = live ? a.iq[b + tt + T * i] : make_double2(0.0, 0.0);
+            for (int i = 0; i < 8; ++i) v[i] = live ? stream_sample(a, b + tt + T * i) : make_double2(0.0, 0.0);
             fft_block<LOGT, -1>(v, tt, lds_tw, fftb + g * N);
             double tot = 0.0, sine = 0.0;
 #pragma unroll
@@ -784,8 +796,7 @@ __global__ void gather_kernel(GatherArgs a)
     const long s = a.starts[f];
     double2* d = a.dst + f * a.span;
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < a.span; i += (long)gridDim.x * blockDim.x) {
-        const long j = s + i;
-        d[i] = (j >= 0 && j < a.n) ? a.iq[j] : make_double2(0.0, 0.0);
+        d[i] = stream_sample(a, s + i);
     }
 }
 

@@ -73,6 +73,7 @@ struct ChanArgs {
 
 struct WalkArgs {
     const double2* iq;          // stream
+    const short2* iq16;         // or: complex<int16> stream (exact int16 -> double on load)
     long n;
     const double2* t2tw;        // T2sin_size forward twiddles
     int a1, b1, a2, b2;         // T2 mask bands
@@ -92,6 +93,7 @@ struct WalkArgs {
 
 struct GatherArgs {
     const double2* iq;
+    const short2* iq16;         // or: complex<int16> stream, converted into dst
     long n;
     const long* starts;         // frame f copies [starts[f], starts[f] + span)
     long nframes, span;

@@ -82,6 +82,7 @@ SIGNATURES = {
     "ofdm_tx_modulate": (_I, [_V, _V, _SZ, _V, _SZ, _V, C.POINTER(Channel), _V]),
     "ofdm_tx_frames": (_I, [_V, _V, _SZ, _V, _V, _V]),
     "ofdm_rx_demod": (_I, [_V, _V, _SZ, _SZ, _V, _SZ, _V, _V, _V, _V, _V]),
+    "ofdm_rx_demod_i16": (_I, [_V, _V, _SZ, _SZ, _V, _SZ, _V, _V, _V, _V, _V]),
     "ofdm_demap": (_I, [_V, _V, _SZ, _V, _V]),
     "ofdm_map": (_I, [_V, _V, _SZ, _V, _V]),
     "ofdm_fft_write": (_I, [_V, _V, _SZ, _V, _V]),
@@ -99,6 +100,7 @@ SIGNATURES = {
     "ofdm_chan_estimate": (_I, [_V, _V, _SZ, _SZ, _V, _SZ, _V]),
     "ofdm_sync_frames": (_I, [_V, _V, _SZ, _SZ, _I, _V, _V, _V, _V]),
     "ofdm_rx_stream": (_I, [_V, _V, _SZ, _SZ, _L, _V, _V, _V, _V, C.POINTER(_SZ), _V]),
+    "ofdm_rx_stream_i16": (_I, [_V, _V, _SZ, _SZ, _L, _V, _V, _V, _V, C.POINTER(_SZ), _V]),
 }
 
 _lib = None
@@ -225,6 +227,14 @@ class Modem:
                                   _ptr(constell_out), _ptr(bytes_out), _ptr(ref), _ptr(bit_errors),
                                   _stream(stream)))
 
+    def rx_i16(self, iq16, nframes: int, frame_stride: int | None = None, chan=None, chan_stride: int = 0,
+               constell_out=None, bytes_out=None, ref=None, bit_errors=None, stream=None):
+        """rx on complex<int16> wire samples (frame_stride in complex samples)."""
+        stride = self.geo.message_len if frame_stride is None else frame_stride
+        check(lib().ofdm_rx_demod_i16(self.h, _ptr(iq16), nframes, stride, _ptr(chan), chan_stride,
+                                      _ptr(constell_out), _ptr(bytes_out), _ptr(ref), _ptr(bit_errors),
+                                      _stream(stream)))
+
     def demap(self, points, n: int, bytes_out, stream=None):
         check(lib().ofdm_demap(self.h, _ptr(points), n, _ptr(bytes_out), _stream(stream)))
 
@@ -288,6 +298,14 @@ class Modem:
         m = C.c_size_t()
         check(lib().ofdm_rx_stream(self.h, _ptr(iq), n, max_frames, chunk, _ptr(pb_out), _ptr(bytes_out),
                                    _ptr(constell_out), _ptr(cfo_out), C.byref(m), _stream(stream)))
+        return m.value
+
+    def rx_stream_i16(self, iq16, n: int, max_frames: int, pb_out=None, bytes_out=None, constell_out=None,
+                      cfo_out=None, chunk: int = 0, stream=None) -> int:
+        """rx_stream on n complex<int16> wire samples."""
+        m = C.c_size_t()
+        check(lib().ofdm_rx_stream_i16(self.h, _ptr(iq16), n, max_frames, chunk, _ptr(pb_out), _ptr(bytes_out),
+                                       _ptr(constell_out), _ptr(cfo_out), C.byref(m), _stream(stream)))
         return m.value
 
     def sync_frames(self, frames, nframes: int, frame_stride: int, stages: int = SYNC_ALL,

@@ -168,6 +168,17 @@ int ofdm_rx_demod(ofdm_ctx* ctx, const double* iq, size_t nframes, size_t frame_
                   const uint8_t* ref_bytes, unsigned long long* bit_errors,
                   void* stream);
 
+/* ofdm_rx_demod on wire-format input: iq16 = complex<int16> samples (4-byte
+ * aligned, device), same frame indexing (FRAME_FORM::from_sdr_int16_buf). The
+ * int16 -> double conversion of FRAME_FORM::form_int16_to_double
+ * (Frame.hpp:472-481) is exact and fused into the load, so results equal
+ * ofdm_rx_demod on the converted samples bit for bit, at 4 B/sample input. */
+int ofdm_rx_demod_i16(ofdm_ctx* ctx, const int16_t* iq16, size_t nframes, size_t frame_stride,
+                      const double* chan, size_t chan_stride,
+                      double* constell_out, uint8_t* bytes_out,
+                      const uint8_t* ref_bytes, unsigned long long* bit_errors,
+                      void* stream);
+
 /* Modulation::demod alone on n points (modulation.cpp:53-87): clamps `points`
  * IN PLACE for QAM (as the reference does) and writes n*k/8 bytes (rounded up,
  * last byte left-aligned as bit_stream_converter pads). Device pointers. */
@@ -282,6 +293,12 @@ int ofdm_sync_frames(ofdm_ctx* ctx, double* frames, size_t nframes, size_t frame
 int ofdm_rx_stream(ofdm_ctx* ctx, const double* iq, size_t n, size_t max_frames, long chunk,
                    long* pb_out, uint8_t* bytes_out, double* constell_out, double* cfo_out,
                    size_t* nframes_out, void* stream);
+/* ofdm_rx_stream on the SDR's wire format (rx.cpp's from_sdr_int16_buf):
+ * iq16 = n complex<int16> samples (device, 4-byte aligned), converted exactly
+ * on load; results equal ofdm_rx_stream on the converted stream. */
+int ofdm_rx_stream_i16(ofdm_ctx* ctx, const int16_t* iq16, size_t n, size_t max_frames, long chunk,
+                       long* pb_out, uint8_t* bytes_out, double* constell_out, double* cfo_out,
+                       size_t* nframes_out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -14,7 +14,8 @@ def golden():
         meta = json.load(f)
     g = dict(meta)
     g["source"] = np.load(os.path.join(GOLDEN_DIR, "source_bin.npy"))
-    d = np.load(os.path.join(GOLDEN_DIR, "data_bin_i16.npz"))["iq"].astype(np.float64)
+    g["data_i16"] = np.load(os.path.join(GOLDEN_DIR, "data_bin_i16.npz"))["iq"]  # interleaved complex<int16>
+    d = g["data_i16"].astype(np.float64)
     g["data"] = d[0::2] + 1j * d[1::2]
     g["t2_corr"] = np.load(os.path.join(GOLDEN_DIR, "t2_sin_corr.npy"))
     g["phases"] = np.load(os.path.join(GOLDEN_DIR, "phases.npy"))

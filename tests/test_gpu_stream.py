@@ -122,3 +122,69 @@ def test_stream_edges():
     cut = want[-1] + g["preamble_len"] + g["message_len"] - 1
     nf2, pbs2, *_ = run_stream(D, x[:cut])
     assert np.array_equal(pbs2, O.stream_walk(D, x[:cut])) and nf2 == len(want) - 1
+
+
+def to_i16(x):
+    """complex<double> -> interleaved complex<int16> (values already integral or rounded here)."""
+    r = np.empty(2 * len(x), np.int16)
+    r[0::2] = np.clip(np.round(x.real), -32768, 32767)
+    r[1::2] = np.clip(np.round(x.imag), -32768, 32767)
+    return r
+
+
+def run_stream_i16(cfg, x16, max_frames=4096, chunk=0):
+    m = modem(cfg)
+    g = O.geometry(cfg)
+    n = len(x16) // 2
+    pbs = torch.full((max_frames,), -1, dtype=torch.int64, device="cuda")
+    out = torch.zeros((max_frames * g["bytes_per_frame"],), dtype=torch.uint8, device="cuda")
+    cons = torch.zeros((max_frames * g["npts"],), dtype=torch.complex128, device="cuda")
+    nf = m.rx_stream_i16(dev(x16), n, max_frames, pb_out=pbs, bytes_out=out, constell_out=cons, chunk=chunk)
+    k = min(nf, max_frames)
+    return nf, host(pbs)[:k], host(out).reshape(max_frames, -1)[:k], host(cons).reshape(max_frames, -1)[:k]
+
+
+def test_stream_i16_replays_reference_wire_capture():
+    """data.bin as the SDR delivered it (complex<int16>): rx_stream_i16 fuses
+    form_int16_to_double and equals the f64 path bit for bit."""
+    nf, pbs, out, cons = run_stream_i16(G, GD["data_i16"])
+    nf2, pbs2, out2, cons2, _ = run_stream(G, GD["data"])
+    assert nf == nf2 == 2 and np.array_equal(pbs, pbs2) and list(pbs) == list(GD["preamble_begin"])
+    assert np.array_equal(out, out2) and np.array_equal(cons, cons2)
+    assert np.array_equal(out[0], GD["payload"])
+
+
+def test_stream_i16_synthetic_equals_f64_path():
+    x, _ = impaired_stream(D, 20, seed=8)
+    x16 = to_i16(x * 200.0)  # the wire scaling of FRAME_FORM::get_int16 (mult)
+    xd = x16[0::2].astype(np.float64) + 1j * x16[1::2].astype(np.float64)
+    got = run_stream_i16(D, x16, chunk=7000)
+    ref = run_stream(D, xd, chunk=7000)
+    assert got[0] == ref[0] and got[0] >= 10
+    for a, b in zip(got[1:], ref[1:4]):
+        assert np.array_equal(a, b)
+    check_against_oracle(D, xd, ref)
+
+
+@pytest.mark.parametrize("name,cfg", [("B", B), ("D", D)])
+def test_rx_i16_equals_rx_on_converted_samples(name, cfg):
+    m = modem(cfg)
+    g = O.geometry(cfg)
+    nf = 64
+    data = payload(nf * g["bytes_per_frame"], seed=5)
+    d = dev(data)
+    iq = torch.empty((nf * g["message_len"],), dtype=torch.complex128, device="cuda")
+    iq16 = torch.empty((2 * nf * g["message_len"],), dtype=torch.int16, device="cuda")
+    m.tx(d, nf, iq, iq16_out=iq16)  # FRAME_FORM::get_int16 wire samples
+    conv = torch.complex(iq16[0::2].double(), iq16[1::2].double())
+    outs = []
+    for fn, src in ((m.rx_i16, iq16), (m.rx, conv)):
+        cons = torch.zeros((nf * g["npts"],), dtype=torch.complex128, device="cuda")
+        out = torch.zeros((nf * g["bytes_per_frame"],), dtype=torch.uint8, device="cuda")
+        errs = torch.zeros((1,), dtype=torch.int64, device="cuda")
+        fn(src, nf, constell_out=cons, bytes_out=out, ref=d, bit_errors=errs)
+        outs.append((host(cons), host(out), int(host(errs)[0])))
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    assert outs[0][2] == 0 and np.array_equal(outs[0][1], data)
+    ocons, oout, _ = O.rx_batch(cfg, host(conv), nf, g["message_len"])
+    assert rel_err(outs[0][0], ocons) < 1e-9 and np.array_equal(outs[0][1], oout)
