@@ -53,6 +53,9 @@ def main():
             "rx(constell+bytes+ber)": (lambda: m.rx(iq, nf, constell_out=cons, bytes_out=out, ref=data,
                                                    bit_errors=errs), rx_b + nf * S * D * k // 8),
             "rx(bytes)": (lambda: m.rx(iq, nf, bytes_out=out), nf * S * (16 * N + D * k // 8)),
+            "rx_i16(constell+bytes+ber)": (lambda: m.rx_i16(iq16, nf, constell_out=cons, bytes_out=out, ref=data,
+                                                           bit_errors=errs),
+                                          nf * S * (4 * N + 16 * D + D * k // 8) + nf * S * D * k // 8),
         }
         # alternating tx -> rx (the bench step): time each kernel of the pair
         def alt(noise):
