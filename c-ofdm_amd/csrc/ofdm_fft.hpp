@@ -199,9 +199,35 @@ struct FftShape {
 
 // One Stockham pass, radix R, input span NS. v[i] holds in[t + T*i].
 // Twiddle powers w^r, r < R, of w = W_N^(k*N/(NS*R)) from the LDS table.
+// Base twiddles w = W_N^(k*N/(NS*R)) of a pass, one per butterfly of this
+// thread (B = 8/R of them). Data independent: the streaming FFT fetches them
+// before the barrier that precedes the pass.
 template <int LOGN, int R, int NS, int SIGN>
-__device__ __forceinline__ void stockham_pass(double2 (&v)[8], int t, const double2* __restrict__ lds_tw,
-                                              double2* __restrict__ lds)
+struct PassTw {
+    double2 w[8 / R];
+};
+
+template <int LOGN, int R, int NS, int SIGN>
+__device__ __forceinline__ PassTw<LOGN, R, NS, SIGN> pass_twiddles(int t, const double2* __restrict__ lds_tw)
+{
+    constexpr int N = 1 << LOGN, T = N / 8, B = 8 / R;
+    PassTw<LOGN, R, NS, SIGN> tw;
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+        if constexpr (NS > 1) {
+            const int k = (t + T * u) & (NS - 1);
+            double2 w1 = tw_get<LOGN>(lds_tw, k * (N / (NS * R)));
+            if (SIGN > 0) w1.y = -w1.y;
+            tw.w[u] = w1;
+        }
+    }
+    return tw;
+}
+
+// One Stockham pass with given base twiddles (see stockham_pass).
+template <int LOGN, int R, int NS, int SIGN>
+__device__ __forceinline__ void stockham_apply(double2 (&v)[8], int t, const PassTw<LOGN, R, NS, SIGN>& tw,
+                                               double2* __restrict__ lds)
 {
     constexpr int N = 1 << LOGN, T = N / 8, B = 8 / R;
 #pragma unroll
@@ -209,10 +235,9 @@ __device__ __forceinline__ void stockham_pass(double2 (&v)[8], int t, const doub
         const int b = t + T * u;
         const int k = b & (NS - 1);
         if constexpr (NS > 1) {
-            double2 w1 = tw_get<LOGN>(lds_tw, k * (N / (NS * R)));
-            if (SIGN > 0) w1.y = -w1.y;
             // running power w^r (two live twiddles: the register window of the
             // streaming kernels leaves no room for all seven)
+            const double2 w1 = tw.w[u];
             double2 w = w1;
             v[u + B] = cmul(v[u + B], w1);
 #pragma unroll
@@ -240,6 +265,15 @@ __device__ __forceinline__ void stockham_pass(double2 (&v)[8], int t, const doub
             for (int r = 0; r < R; ++r) lds[lds_swz(idxD + r * NS)] = v[u + r * B];
         }
     }
+}
+
+// One Stockham pass, radix R, input span NS. v[i] holds in[t + T*i].
+// Twiddle powers w^r, r < R, of w = W_N^(k*N/(NS*R)) from the LDS table.
+template <int LOGN, int R, int NS, int SIGN>
+__device__ __forceinline__ void stockham_pass(double2 (&v)[8], int t, const double2* __restrict__ lds_tw,
+                                              double2* __restrict__ lds)
+{
+    stockham_apply<LOGN, R, NS, SIGN>(v, t, pass_twiddles<LOGN, R, NS, SIGN>(t, lds_tw), lds);
 }
 
 template <int LOGN>
@@ -312,9 +346,10 @@ __device__ __forceinline__ void fft_pp_tail(double2 (&v)[8], int t, const double
         constexpr bool is8 = PASS < S::NPASS8;
         constexpr int R = is8 ? 8 : (1 << S::REM);
         constexpr int NS = 1 << (3 * PASS);
+        const auto tw = pass_twiddles<LOGN, R, NS, SIGN>(t, lds_tw);  // constant table: before the barrier
         lds_barrier();  // pass PASS-1 fully written to b1
         lds_load8<LOGN>(v, t, b1);
-        stockham_pass<LOGN, R, NS, SIGN>(v, t, lds_tw, b0);
+        stockham_apply<LOGN, R, NS, SIGN>(v, t, tw, b0);
         fft_pp_tail<LOGN, PASS + 1, SIGN>(v, t, lds_tw, b1, b0, hook);
     } else {
         hook();         // e.g. publish the next symbol's LDS inputs under the same barrier

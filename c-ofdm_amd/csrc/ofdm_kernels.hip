@@ -378,7 +378,8 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
     const int pbin = a.tab.pilot_swz[t];
     SymbolRegs<LOGN, I16> pf;
     pf.load(a, x0, t);
-    if constexpr (kTwSplit) tw_store<LOGN>(twp, lds_tw);  // read after pass 0's barrier
+    if constexpr (kTwSplit) tw_store<LOGN>(twp, lds_tw);
+    lds_barrier();  // twiddle table visible: fft_pp reads a pass's twiddles before its barrier
 
     double2 y[SW][RX_DPT];
     double2* first = bufA;
