@@ -40,14 +40,43 @@ __device__ __forceinline__ int symbol_bits(const uint8_t* __restrict__ b, long n
 // Modulation::demod decision for one point (modulation.cpp:62-84): BPSK
 // re+im > 0; QAM clamp to [-1,1] then uint8((v+1)*str_size_1 + 0.5) per axis,
 // idx = re | im*str_size. Separate roundings (no FMA) as on x86-64.
+// The clamp is v_max/v_min: equal to the reference's compare chain for every
+// non-NaN value; a NaN (degenerate all-zero pilots) decides 0 either way
+// (chain: cvt(NaN) = 0; min/max: clamps to -1, then uint8(0.5) = 0).
 __device__ __forceinline__ int decide(double2 z, int k, double s1, int m)
 {
     if (k == 1) return (z.x + z.y) > 0.0;
-    const double re = z.x < -1.0 ? -1.0 : (1.0 < z.x ? 1.0 : z.x);
-    const double im = z.y < -1.0 ? -1.0 : (1.0 < z.y ? 1.0 : z.y);
+    const double re = __builtin_fmin(__builtin_fmax(z.x, -1.0), 1.0);
+    const double im = __builtin_fmin(__builtin_fmax(z.y, -1.0), 1.0);
     const int ire = (uint8_t)(int)__dadd_rn(__dmul_rn(__dadd_rn(re, 1.0), s1), 0.5);
     const int iim = (uint8_t)(int)__dadd_rn(__dmul_rn(__dadd_rn(im, 1.0), s1), 0.5);
     return (ire | (iim * m)) & 0xff;
+}
+
+// Four output bytes (one little-endian word) from 32/K consecutive K-bit
+// decisions held one per byte in LDS (MSB-first within each byte, as
+// bit_stream_converter(8, K, ...), modulation.cpp:90-125).
+template <int K>
+__device__ __forceinline__ uint32_t pack_word(const uint8_t* __restrict__ dec)
+{
+    constexpr int PER = 8 / K;  // decisions per output byte
+    constexpr int NW = 8 / K;   // 32-bit LDS words holding the 32/K decisions (dec is 32/K-byte aligned)
+    uint32_t d[NW];
+    const uint32_t* d32 = reinterpret_cast<const uint32_t*>(dec);
+#pragma unroll
+    for (int i = 0; i < NW; ++i) d[i] = d32[i];
+    uint32_t word = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        uint32_t byte = 0;
+#pragma unroll
+        for (int r = 0; r < PER; ++r) {
+            const int idx = b * PER + r;
+            byte = (byte << K) | ((d[idx >> 2] >> (8 * (idx & 3))) & 0xffu);
+        }
+        word |= byte << (8 * b);
+    }
+    return word;
 }
 
 __device__ __forceinline__ double2 clamp_point(double2 z)
@@ -474,6 +503,25 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
         }
     };
 
+    // word-wise packing: k in {1,2,4,8}, whole words, 4-byte aligned outputs
+    const bool by_word = (a.k == 1 || a.k == 2 || a.k == 4 || a.k == 8) && (bpf & 3) == 0 &&
+                         ((uintptr_t)a.bytes & 3) == 0 && ((uintptr_t)a.ref & 3) == 0;
+    auto pack_words = [&]() {
+        const int per_word = 32 / a.k;  // decisions per output word
+        for (long w = t; w < bpf / 4; w += T) {
+            const uint8_t* dw = dec + w * per_word;
+            uint32_t word;
+            switch (a.k) {
+                case 1: word = pack_word<1>(dw); break;
+                case 2: word = pack_word<2>(dw); break;
+                case 4: word = pack_word<4>(dw); break;
+                default: word = pack_word<8>(dw); break;
+            }
+            if (a.bytes) reinterpret_cast<uint32_t*>(a.bytes + f * bpf)[w] = word;
+            if (a.ref) errs += __popc(word ^ reinterpret_cast<const uint32_t*>(a.ref + f * bpf)[w]);
+        }
+    };
+
     if constexpr (!STAGED) {
 #pragma unroll
         for (int w = 0; w < SW; ++w) {
@@ -484,7 +532,10 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
             }
         }
         __syncthreads();
-        pack(0, bpf, 0);
+        if (by_word)
+            pack_words();
+        else
+            pack(0, bpf, 0);
     } else {
         const long bps = (long)D * a.k / 8;  // bytes per symbol (host checks D*k % 8 == 0)
         for (int s = 0; s < S; ++s) {
