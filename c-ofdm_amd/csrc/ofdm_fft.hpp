@@ -37,12 +37,32 @@ __device__ __forceinline__ double2 cmul(double2 a, double2 b)
     return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
 
+// Separately rounded FP64 operations, as the reference's x86-64 build (no
+// FMA) computes them. HIP's __dmul_rn/__dadd_rn are plain operators that the
+// default -ffp-contract=fast-honor-pragmas would fuse into v_fma_f64; the
+// pragma drops the `contract` flag on these operations, even after inlining.
+__device__ __forceinline__ double mul_rn(double a, double b)
+{
+#pragma clang fp contract(off)
+    return a * b;
+}
+__device__ __forceinline__ double add_rn(double a, double b)
+{
+#pragma clang fp contract(off)
+    return a + b;
+}
+__device__ __forceinline__ double sub_rn(double a, double b)
+{
+#pragma clang fp contract(off)
+    return a - b;
+}
+
 // Complex product with the exact rounding of g++'s inline _Complex multiply
 // on x86-64 (no FMA): used where the reference's own arithmetic is mirrored.
 __device__ __forceinline__ double2 cmul_exact(double2 a, double2 b)
 {
-    return make_double2(__dsub_rn(__dmul_rn(a.x, b.x), __dmul_rn(a.y, b.y)),
-                        __dadd_rn(__dmul_rn(a.x, b.y), __dmul_rn(a.y, b.x)));
+    return make_double2(sub_rn(mul_rn(a.x, b.x), mul_rn(a.y, b.y)),
+                        add_rn(mul_rn(a.x, b.y), mul_rn(a.y, b.x)));
 }
 
 // libgcc __divdc3 (Smith's algorithm) for finite operands — what the
@@ -53,14 +73,14 @@ __device__ __forceinline__ double2 cdiv_exact(double2 n, double2 d)
     double x, y;
     if (fabs(c) < fabs(e)) {
         const double ratio = c / e;
-        const double denom = __dadd_rn(__dmul_rn(c, ratio), e);
-        x = __dadd_rn(__dmul_rn(a, ratio), b) / denom;
-        y = __dsub_rn(__dmul_rn(b, ratio), a) / denom;
+        const double denom = add_rn(mul_rn(c, ratio), e);
+        x = add_rn(mul_rn(a, ratio), b) / denom;
+        y = sub_rn(mul_rn(b, ratio), a) / denom;
     } else {
         const double ratio = e / c;
-        const double denom = __dadd_rn(__dmul_rn(e, ratio), c);
-        x = __dadd_rn(__dmul_rn(b, ratio), a) / denom;
-        y = __dsub_rn(b, __dmul_rn(a, ratio)) / denom;
+        const double denom = add_rn(mul_rn(e, ratio), c);
+        x = add_rn(mul_rn(b, ratio), a) / denom;
+        y = sub_rn(b, mul_rn(a, ratio)) / denom;
     }
     return make_double2(x, y);
 }

@@ -48,8 +48,8 @@ __device__ __forceinline__ int decide(double2 z, int k, double s1, int m)
     if (k == 1) return (z.x + z.y) > 0.0;
     const double re = __builtin_fmin(__builtin_fmax(z.x, -1.0), 1.0);
     const double im = __builtin_fmin(__builtin_fmax(z.y, -1.0), 1.0);
-    const int ire = (uint8_t)(int)__dadd_rn(__dmul_rn(__dadd_rn(re, 1.0), s1), 0.5);
-    const int iim = (uint8_t)(int)__dadd_rn(__dmul_rn(__dadd_rn(im, 1.0), s1), 0.5);
+    const int ire = (uint8_t)(int)add_rn(mul_rn(add_rn(re, 1.0), s1), 0.5);
+    const int iim = (uint8_t)(int)add_rn(mul_rn(add_rn(im, 1.0), s1), 0.5);
     return (ire | (iim * m)) & 0xff;
 }
 

@@ -27,6 +27,10 @@
 #include "ofdm_fft.hpp"
 #include "ofdm_sync.hpp"
 
+// The sync chain mirrors the reference's x86-64 arithmetic (no FMA): no
+// contraction in this file (the FFT in ofdm_fft.hpp keeps its FMAs).
+#pragma clang fp contract(off)
+
 namespace ofdm {
 
 namespace {
@@ -38,7 +42,7 @@ __device__ __forceinline__ double2 cconj_mul(double2 a, double2 b)  // conj(a) *
 
 __device__ __forceinline__ double2 cadd_rn(double2 a, double2 b)
 {
-    return make_double2(__dadd_rn(a.x, b.x), __dadd_rn(a.y, b.y));
+    return make_double2(add_rn(a.x, b.x), add_rn(a.y, b.y));
 }
 
 // Block-wide complex / double sums (NT threads, multiple of 64 or < 64).
@@ -216,12 +220,12 @@ __global__ void __launch_bounds__(SYNC_THREADS) find_preamble_kernel(PreambleArg
     // serial running energy, exactly the reference's operation order (Frame.cpp:346-375)
     if (t == 0) {
         double norm = 0.0;
-        for (int i = 0; i < L; ++i) norm = __dadd_rn(norm, __dadd_rn(__dmul_rn(xs[i].x, xs[i].x), __dmul_rn(xs[i].y, xs[i].y)));
+        for (int i = 0; i < L; ++i) norm = add_rn(norm, add_rn(mul_rn(xs[i].x, xs[i].x), mul_rn(xs[i].y, xs[i].y)));
         for (int i = 0; i < C; ++i) {
             normv[i] = norm;
             const double2 p = xs[i + L], q = xs[i];
-            norm = __dadd_rn(norm, __dadd_rn(__dmul_rn(p.x, p.x), __dmul_rn(p.y, p.y)));
-            norm = __dsub_rn(norm, __dadd_rn(__dmul_rn(q.x, q.x), __dmul_rn(q.y, q.y)));
+            norm = add_rn(norm, add_rn(mul_rn(p.x, p.x), mul_rn(p.y, p.y)));
+            norm = sub_rn(norm, add_rn(mul_rn(q.x, q.x), mul_rn(q.y, q.y)));
         }
     }
     // correlation per lag, j = 0..L-1 in order (Frame.cpp:360-363)
@@ -564,9 +568,9 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) chan_kernel(ChanArgs a)
     for (int i = t; i < a.D; i += T) {
         double th;
         if (i < half)
-            th = __dadd_rn(__dmul_rn(b, (double)i), aa);
+            th = add_rn(mul_rn(b, (double)i), aa);
         else
-            th = __dadd_rn(__dadd_rn(__dmul_rn(-b, (double)a.D) / 2, __dmul_rn((double)(i - half), b)), aa);
+            th = add_rn(add_rn(mul_rn(-b, (double)a.D) / 2, mul_rn((double)(i - half), b)), aa);
         double sn, cs;
         sincos(th, &sn, &cs);
         chan[i] = make_double2(cs, sn);
@@ -647,17 +651,17 @@ __device__ int walk_preamble(const WalkArgs& a, long s, double2* xs, const doubl
     for (int i = t; i < C + L; i += WALK_THREADS) {
         const double2 v = stream_sample(a, s + i);
         xs[i] = v;
-        E[i] = __dadd_rn(__dmul_rn(v.x, v.x), __dmul_rn(v.y, v.y));
+        E[i] = add_rn(mul_rn(v.x, v.x), mul_rn(v.y, v.y));
     }
     if (t == 0) *best = INT_MAX;
     __syncthreads();
     if (t == 0) {
         double norm = 0.0;
-        for (int i = 0; i < L; ++i) norm = __dadd_rn(norm, E[i]);
+        for (int i = 0; i < L; ++i) norm = add_rn(norm, E[i]);
         for (int i = 0; i < C; ++i) {
             normv[i] = norm;
-            norm = __dadd_rn(norm, E[i + L]);
-            norm = __dsub_rn(norm, E[i]);
+            norm = add_rn(norm, E[i + L]);
+            norm = sub_rn(norm, E[i]);
         }
     }
     __syncthreads();
