@@ -118,6 +118,7 @@ struct ofdm_ctx {
     int* d_bin_map = nullptr;
     int* d_rx_pack = nullptr;
     int* d_pilot_swz = nullptr;
+    int* d_tx_code = nullptr;
     double2* d_const = nullptr;
     double2* d_const_bpsk = nullptr;
     double2* d_header = nullptr;   // T2 + preamble
@@ -158,6 +159,7 @@ struct ofdm_ctx {
         t.bin_map = d_bin_map;
         t.rx_pack = d_rx_pack;
         t.pilot_swz = d_pilot_swz;
+        t.tx_code = d_tx_code;
         t.constell = bpsk ? d_const_bpsk : d_const;
         return t;
     }
@@ -283,7 +285,7 @@ int ofdm_destroy(ofdm_ctx* c)
     if (!c) return OFDM_OK;
     (void)hipSetDevice(c->device);
     void* ptrs[] = {c->d_tw, c->d_data_bin, c->d_data_slot, c->d_pilot_bin, c->d_bin_map, c->d_rx_pack,
-                    c->d_pilot_swz, c->d_const,
+                    c->d_pilot_swz, c->d_tx_code, c->d_const,
                     c->d_const_bpsk, c->d_header, c->d_preamble, c->d_templ, c->d_modpre, c->d_t2mask,
                     c->d_t2tw, c->d_first, c->d_scratch, c->d_cfo_scratch};
     for (void* q : ptrs)
@@ -397,7 +399,14 @@ int ofdm_create(const ofdm_params* params, int device, ofdm_ctx** out)
         pilot_swz(std::max(c->P, c->N / 8), 0);
     for (int d = 0; d < c->D; ++d) rx_pack[d] = ofdm::lds_swz_host(data_bin[d]) | (data_slot[d] << 16);
     for (int j = 0; j < c->P; ++j) pilot_swz[j] = ofdm::lds_swz_host(pilot[j]);
+    // tx per-bin codes (ofdm_internal.hpp tx_code): data index + 0xff mask, or
+    // the pilot / zero entry of the kernel's LDS point table
+    std::vector<int> tx_code(c->N);
+    for (int b = 0; b < c->N; ++b)
+        tx_code[b] = bin_map[b] >= 0 ? ofdm::tx_code_data(bin_map[b])
+                                     : ofdm::tx_code_fixed(bin_map[b] == -2 ? ofdm::TX_LDS_PILOT : ofdm::TX_LDS_ZERO);
     if ((rc = upload(&c->d_rx_pack, rx_pack)) || (rc = upload(&c->d_pilot_swz, pilot_swz)) ||
+        (rc = upload(&c->d_tx_code, tx_code)) ||
         (rc = upload(&c->d_tw, twiddles(c->N))) || (rc = upload(&c->d_data_bin, data_bin)) ||
         (rc = upload(&c->d_data_slot, data_slot)) || (rc = upload(&c->d_pilot_bin, pilot)) ||
         (rc = upload(&c->d_bin_map, bin_map)) || (rc = upload(&c->d_const, constellation(c->k))) ||

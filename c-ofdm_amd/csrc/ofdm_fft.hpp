@@ -245,7 +245,8 @@ __device__ __forceinline__ PassTw<LOGN, R, NS, SIGN> pass_twiddles(int t, const 
 }
 
 // One Stockham pass with given base twiddles (see stockham_pass).
-template <int LOGN, int R, int NS, int SIGN>
+// WRITE = false: the butterflies' results stay in v (last pass of fft_regs).
+template <int LOGN, int R, int NS, int SIGN, bool WRITE = true>
 __device__ __forceinline__ void stockham_apply(double2 (&v)[8], int t, const PassTw<LOGN, R, NS, SIGN>& tw,
                                                double2* __restrict__ lds)
 {
@@ -273,6 +274,7 @@ __device__ __forceinline__ void stockham_apply(double2 (&v)[8], int t, const Pas
             dft4<SIGN>(v[u], v[u + B], v[u + 2 * B], v[u + 3 * B]);
         else
             dft2<SIGN>(v[u], v[u + B]);
+        if constexpr (!WRITE) continue;
         const int idxD = (b - k) * R + k;
         if constexpr (NS % 64 == 0) {
             // r*NS has zero low 6 bits: the swizzle of idxD carries over, so one
@@ -339,6 +341,44 @@ __device__ __forceinline__ void fft_block(double2 (&v)[8], int t, const double2*
     stockham_pass<LOGN, 8, 1, SIGN>(v, t, lds_tw, lds);
     fft_tail<LOGN, 1, SIGN>(v, t, lds_tw, lds);
     lds_barrier();
+}
+
+// ---------------------------------------------------------------- register output
+// The last Stockham pass (span NS = N/R) writes butterfly b = t + T*u, output
+// r to index b + r*N/R = t + T*(u + r*B): exactly the register v[u + r*B]
+// that holds it. So the final pass needs no LDS write and no re-read: on exit
+// v[i] = X[t + T*i] (natural order, coalesced for a direct HBM store).
+// Single LDS image; the caller must barrier before `lds` is written again
+// (other threads may still be reading the last pass's inputs).
+template <int LOGN, int PASS, int SIGN>
+__device__ __forceinline__ void fft_regs_tail(double2 (&v)[8], int t, const double2* __restrict__ lds_tw,
+                                              double2* __restrict__ lds)
+{
+    using S = FftShape<LOGN>;
+    constexpr int NPASS = S::NPASS8 + (S::REM ? 1 : 0);
+    constexpr bool is8 = PASS < S::NPASS8;
+    constexpr int R = is8 ? 8 : (1 << S::REM);
+    constexpr int NS = 1 << (3 * PASS);
+    constexpr bool LAST = PASS == NPASS - 1;
+    const auto tw = pass_twiddles<LOGN, R, NS, SIGN>(t, lds_tw);  // constant table: before the barrier
+    lds_barrier();  // previous pass fully written
+    lds_load8<LOGN>(v, t, lds);
+    if constexpr (LAST) {
+        stockham_apply<LOGN, R, NS, SIGN, false>(v, t, tw, lds);
+    } else {
+        lds_barrier();  // everyone has read before the image is overwritten
+        stockham_apply<LOGN, R, NS, SIGN>(v, t, tw, lds);
+        fft_regs_tail<LOGN, PASS + 1, SIGN>(v, t, lds_tw, lds);
+    }
+}
+
+template <int LOGN, int SIGN>
+__device__ __forceinline__ void fft_regs(double2 (&v)[8], int t, const double2* __restrict__ lds_tw,
+                                         double2* __restrict__ lds)
+{
+    static_assert(LOGN >= 6 && LOGN <= 12, "N must be 64..4096");
+    stockham_pass<LOGN, 8, 1, SIGN>(v, t, lds_tw, lds);
+    fft_regs_tail<LOGN, 1, SIGN>(v, t, lds_tw, lds);
 }
 
 // ---------------------------------------------------------------- ping-pong

@@ -15,6 +15,7 @@ struct DevTables {
     const int* bin_map;         // N: >=0 data index, -1 unused bin, -2 pilot
     const int* rx_pack;         // max(D, RX_DPT*N/8): lds_swz(data_bin) | data_slot << 16, 0-padded
     const int* pilot_swz;       // max(P, N/8): lds_swz(pilot_bin), 0-padded
+    const int* tx_code;         // N: tx per-bin code (tx_code_data / tx_code_fixed)
     const double2* constell;    // 2^k mapping table (Modulation::constell)
 };
 
@@ -74,6 +75,15 @@ constexpr int RX_SMAX = 8;
 // LDS slot of FFT element e (ofdm_fft.hpp lds_swz), for host-built tables
 inline int lds_swz_host(int e) { return e ^ ((e >> 3) & 7); }
 constexpr int RX_DPT = 4;
+// rx: persistent workgroups per CU (2 x 4 waves: the register window's occupancy)
+constexpr int RX_WG_PER_CU = 2;
+// tx per-bin code: bits 0-12 data index d, bits 13-20 mask applied to its
+// k-bit payload symbol (0xff data, 0 otherwise), bits 21-29 base entry of the
+// tx kernel's LDS point table (0 for data; TX_LDS_PILOT / TX_LDS_ZERO hold the
+// pilot amplitude and 0), so every bin maps as table[(bits(d) & mask) + base].
+constexpr int TX_LDS_PILOT = 256, TX_LDS_ZERO = 257;
+inline int tx_code_data(int d) { return d | (0xff << 13); }
+inline int tx_code_fixed(int entry) { return entry << 21; }
 // tx: persistent grid-stride launch size (symbols per workgroup = nsym / grid)
 constexpr long TX_MAX_GRID = 4096;
 

@@ -176,6 +176,28 @@ __device__ __forceinline__ double block_sum(double v, double* red)
     }
 }
 
+// block_sum with LDS-only barriers: leaves in-flight vector-memory loads and
+// stores outstanding (a __syncthreads() would drain them).
+template <int NT>
+__device__ __forceinline__ double block_sum_lds(double v, double* red)
+{
+#pragma unroll
+    for (int o = (NT >= 64 ? 32 : NT / 2); o > 0; o >>= 1) v += __shfl_xor(v, o);
+    constexpr int NW = (NT + 63) / 64;
+    if constexpr (NW == 1) {
+        return v;
+    } else {
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        if (lane == 0) red[w] = v;
+        lds_barrier();
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) s += red[i];
+        lds_barrier();  // red is rewritten by the next reduction
+        return s;
+    }
+}
+
 template <int NT>
 __device__ __forceinline__ unsigned long long block_sum_u64(unsigned long long v, double* red)
 {
@@ -201,7 +223,9 @@ __device__ __forceinline__ unsigned long long block_sum_u64(unsigned long long v
 // symbol's payload bytes are fetched into registers while this one is
 // transformed and written.
 // POINTS = true: FFT_FORM::write on given constellation points (no payload bytes).
-template <int LOGN, bool POINTS>
+// NOISE / I16: fused AWGN and int16 wire output compiled in (a.noise_scale > 0,
+// a.iq16 != nullptr), so each variant gets its own register allocation.
+template <int LOGN, bool POINTS, bool NOISE, bool I16>
 __global__ void __launch_bounds__((1 << LOGN) / 8) tx_kernel(TxArgs a)
 {
     using FS = FftShape<LOGN>;
@@ -209,39 +233,73 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) tx_kernel(TxArgs a)
     extern __shared__ double2 smem[];
     double2* fft = smem;
     double2* lds_tw = smem + FS::PADN;
-    double2* lds_const = lds_tw + TwLds<LOGN>::SIZE;                            // 2^k points
-    uint8_t* sbytes = reinterpret_cast<uint8_t*>(lds_const + 256);              // one symbol's payload
+    double2* lds_const = lds_tw + TwLds<LOGN>::SIZE;  // 2^k points, then pilot (TX_LDS_PILOT) and 0 (TX_LDS_ZERO)
+    uint8_t* sbytes = reinterpret_cast<uint8_t*>(lds_const + TX_LDS_ZERO + 1);  // one symbol's payload (N bytes)
     const int t = threadIdx.x;
     load_twiddles<LOGN>(a.tab.tw, lds_tw, t, T);
     for (int i = t; i < (1 << a.k); i += T) lds_const[i] = a.tab.constell[i];
+    if (t == 0) {
+        lds_const[TX_LDS_PILOT] = make_double2(a.pilot_ampl, 0.0);
+        lds_const[TX_LDS_ZERO] = make_double2(0.0, 0.0);
+    }
 
-    // FFT_FORM::write layout: bin -> data index / pilot / unused (Frame.cpp:31-44,54-62)
-    int kind[8];
+    // FFT_FORM::write layout (Frame.cpp:31-44,54-62) as per-bin codes: data
+    // index, payload-symbol mask, table base (ofdm_internal.hpp tx_code)
+    int code[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) kind[i] = a.tab.bin_map[t + T * i];
+    for (int i = 0; i < 8; ++i) code[i] = a.tab.tx_code[t + T * i];
 
     const long nsym = a.nframes * a.S;
     const int k = a.k;
     const int bps = a.D * k / 8;  // payload bytes per symbol (host checks D*k % 8 == 0)
-    const double2 pil = make_double2(a.pilot_ampl, 0.0);
     const int L = N + a.cp;
     auto sym_bytes = [&](long sym) {
         const long f = sym / a.S;
         return a.bytes + f * a.bytes_per_frame + (sym - f * a.S) * bps;
     };
+    // Payload prefetch, written to LDS only after the FFT so the loads' latency
+    // hides behind it: 32-bit words t and t + T when every symbol's payload is
+    // word aligned (bps <= N bytes = 2T words), else bytes t + T*r. Indices are
+    // clamped and the whole N-byte stage is rewritten (bytes past bps are never
+    // decoded), so neither side needs per-lane guards.
+    const bool by_word = (bps & 3) == 0 && (a.bytes_per_frame & 3) == 0 && ((uintptr_t)a.bytes & 3) == 0;
+    const int nwords = bps >> 2;
+    const int wi0 = t < nwords ? t : 0, wi1 = t + T < nwords ? t + T : 0;
+    uint32_t nb[8];
+    auto fetch = [&](long s) {
+        const uint8_t* src = sym_bytes(s);
+        if (by_word) {
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(src);
+            nb[0] = w[wi0];
+            nb[1] = w[wi1];
+        } else {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) nb[r] = src[t + T * r < bps ? t + T * r : 0];
+        }
+    };
+    auto publish = [&]() {
+        if (by_word) {
+            uint32_t* w = reinterpret_cast<uint32_t*>(sbytes);
+            w[t] = nb[0];
+            w[t + T] = nb[1];
+        } else {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) sbytes[t + T * r] = (uint8_t)nb[r];
+        }
+    };
 
-    // Coalesced payload prefetch: thread t holds bytes t + T*r of the next
-    // symbol (bps <= N = 8T); they are written to LDS only at the end of the
-    // iteration, so the loads' latency hides behind the FFT.
-    uint8_t nb[8];
     long sym = blockIdx.x;
     if (!POINTS && sym < nsym) {
-        const uint8_t* src = sym_bytes(sym);
-#pragma unroll
-        for (int r = 0; r < 8; ++r)
-            if (t + T * r < bps) sbytes[t + T * r] = src[t + T * r];
+        fetch(sym);
+        publish();
     }
     lds_barrier();  // twiddle table + first payload visible
+
+    // CP samples n in [N-cp, N) are registers v[i], i >= 8 - cp/T, of the same
+    // thread when cp is a multiple of T (the configs' cp = N/4 = 2T)
+    const bool cp_reg = (a.cp % T) == 0;
+    const int i_cp = 8 - a.cp / T;
+    const int kmask = (1 << k) - 1;
 
     // (frame, symbol) of `sym`, advanced incrementally (no 64-bit division in the loop)
     const long gstep_f = gridDim.x / a.S;
@@ -249,75 +307,81 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) tx_kernel(TxArgs a)
     long f = sym / a.S;
     int s = (int)(sym - f * a.S);
     for (; sym < nsym; sym += gridDim.x) {
-        // Modulation::mod: k-bit symbol -> constellation point (modulation.cpp:39-50)
+        // Modulation::mod: k-bit symbol -> constellation point (modulation.cpp:39-50);
+        // pilots = pilot_ampl, unused bins 0 (Frame.cpp:56-62)
         double2 v[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            if (POINTS && kind[i] >= 0) {
-                v[i] = a.points[sym * a.D + kind[i]];
-            } else if (kind[i] >= 0) {
-                const int bit = kind[i] * k;
-                const int byte = bit >> 3, off = bit & 7;
-                const int w = ((int)sbytes[byte] << 8) | (off + k > 8 ? (int)sbytes[byte + 1] : 0);
-                v[i] = lds_const[(w >> (16 - off - k)) & ((1 << k) - 1)];
+            const int d = code[i] & 0x1fff, m = (code[i] >> 13) & 0xff, base = code[i] >> 21;
+            if constexpr (POINTS) {
+                v[i] = m ? a.points[sym * a.D + d] : lds_const[base];
             } else {
-                v[i] = kind[i] == -2 ? pil : make_double2(0.0, 0.0);
+                const int bit = d * k;
+                const int byte = bit >> 3, off = bit & 7;
+                const int w = ((int)sbytes[byte] << 8) | (int)sbytes[byte + 1];
+                v[i] = lds_const[((w >> (16 - off - k)) & kmask & m) + base];
             }
         }
         const long nxt = sym + gridDim.x;
-        if constexpr (!POINTS) {
-            const uint8_t* nsrc = sym_bytes(nxt < nsym ? nxt : sym);
-#pragma unroll
-            for (int r = 0; r < 8; ++r) nb[r] = nsrc[t + T * r < bps ? t + T * r : 0];
-        }
+        if constexpr (!POINTS) fetch(nxt < nsym ? nxt : sym);
 
-        fft_block<LOGN, +1>(v, t, lds_tw, fft);
+        // unnormalised backward DFT (Frame.cpp:64); v[i] = x[t + T*i] on exit
+        fft_regs<LOGN, +1>(v, t, lds_tw, fft);
         // Publish the next payload now, before this symbol's stores: on gfx9
         // vmcnt also counts stores, so a wait on these loads placed after the
         // stores would drain them every symbol. Every thread has mapped this
         // symbol (FFT barriers since), so the single stage can be rewritten.
-        if constexpr (!POINTS) {
-#pragma unroll
-            for (int r = 0; r < 8; ++r)
-                if (t + T * r < bps) sbytes[t + T * r] = nb[r];
-        }
+        if constexpr (!POINTS) publish();
 
         // body / sqrt(N) after a CP copy of its last cp samples (Frame.cpp:66-68,191-197)
         const long base = f * a.frame_stride + a.msg_offset + (long)s * L;
         double2* out = a.iq + base;
-        int16_t* out16 = a.iq16 ? a.iq16 + 2 * base : nullptr;
+        int16_t* out16 = I16 ? a.iq16 + 2 * base : nullptr;
         const unsigned long long g0 = a.sample_offset + (unsigned long long)sym * L;
-        const AwgnRun run = awgn_run(awgn_key(a.seed), g0);
-        for (int j = t; j < L; j += T) {
-            const int n = j < a.cp ? N - a.cp + j : j - a.cp;
-            double2 z = fft[lds_swz(n)];
+        const AwgnRun run = NOISE ? awgn_run(awgn_key(a.seed), g0) : AwgnRun{};
+        auto emit = [&](int j, double2 z) {
             z.x *= a.inv_sqrt_n;
             z.y *= a.inv_sqrt_n;
-            if (out16) {
+            if constexpr (I16) {
                 const uint32_t w = (uint16_t)to_int16(z.x * a.mult) | ((uint32_t)(uint16_t)to_int16(z.y * a.mult) << 16);
                 __builtin_nontemporal_store(w, reinterpret_cast<uint32_t*>(out16 + 2 * j));
             }
-            if (a.noise_scale > 0.0) {
+            if constexpr (NOISE) {
                 const double2 w = awgn_sample(run, (uint32_t)j, a.noise_scale);
                 z.x += w.x;
                 z.y += w.y;
             }
             store_nt(out + j, z);
+        };
+        if (cp_reg) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (i >= i_cp) emit(t + T * i - (N - a.cp), v[i]);
+        } else {
+            // general cp: the tail of the symbol through the LDS image
+            lds_barrier();  // every thread has read the last pass's inputs
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (t + T * i >= N - a.cp) fft[lds_swz(t + T * i)] = v[i];
+            lds_barrier();
+            for (int j = t; j < a.cp; j += T) emit(j, fft[lds_swz(N - a.cp + j)]);
         }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) emit(a.cp + t + T * i, v[i]);
         // [T2 | preamble] header of full FRAME_FORM buffers (Frame.cpp:219,228-229)
         if (a.header && s == 0) {
             double2* fr = a.iq + f * a.frame_stride;
-            int16_t* fr16 = a.iq16 ? a.iq16 + 2 * f * a.frame_stride : nullptr;
+            int16_t* fr16 = I16 ? a.iq16 + 2 * f * a.frame_stride : nullptr;
             for (int j = t; j < a.header_len; j += T) {
                 const double2 z = a.header[j];
                 fr[j] = z;
-                if (fr16) {
+                if constexpr (I16) {
                     fr16[2 * j] = to_int16(z.x * a.mult);
                     fr16[2 * j + 1] = to_int16(z.y * a.mult);
                 }
             }
         }
-        lds_barrier();  // next payload visible; fft[] output reads precede the next pass 0
+        lds_barrier();  // next payload visible; the last pass's LDS reads precede the next pass 0
         s += gstep_s;
         f += gstep_f;
         if (s >= a.S) {
@@ -370,6 +434,61 @@ struct SymbolRegs<LOGN, true> {
     }
 };
 
+// Symbol 0 of a frame streams HBM -> LDS by LDS-DMA (global_load_lds_dwordx4,
+// or _dword for complex<int16>), issued while the previous frame's epilogue
+// runs: no registers stay live across the epilogue for it. Lane l of wave w0
+// lands element w0 + T*i + l, so each thread later reads only what its own
+// wave fetched (a vmcnt wait, no barrier). Inline asm (MI355X guide LDS-DMA
+// recipe: M0 = wave-uniform LDS byte address): the compiler does not track
+// the transfer, so the reader issues its own `s_waitcnt vmcnt(0)`.
+template <int LOGN, bool I16>
+__device__ __forceinline__ void dma_symbol(const RxArgs& a, long off, void* stage, int t)
+{
+    constexpr int T = (1 << LOGN) / 8;
+    constexpr int ESZ = I16 ? 4 : 16;
+    const int w0 = t & ~63;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int e0 = w0 + T * i;  // wave-uniform
+        const char* g = I16 ? reinterpret_cast<const char*>(a.iq16 + off + e0 + (t & 63))
+                            : reinterpret_cast<const char*>(a.iq + off + e0 + (t & 63));
+        const unsigned lds = __builtin_amdgcn_readfirstlane(
+            (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)((char*)stage + (size_t)e0 * ESZ));
+        unsigned keep;
+        if constexpr (I16)
+            asm volatile(
+                "s_mov_b32 %0, m0\n\t"
+                "s_mov_b32 m0, %2\n\t"
+                "s_nop 0\n\t"
+                "global_load_lds_dword %1, off nt\n\t"
+                "s_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(g), "s"(lds)
+                : "memory");
+        else
+            asm volatile(
+                "s_mov_b32 %0, m0\n\t"
+                "s_mov_b32 m0, %2\n\t"
+                "s_nop 0\n\t"
+                "global_load_lds_dwordx4 %1, off nt\n\t"
+                "s_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(g), "s"(lds)
+                : "memory");
+    }
+}
+
+template <int LOGN, bool I16>
+__device__ __forceinline__ double2 stage_get(const void* stage, int e)
+{
+    if constexpr (I16) {
+        const int r = reinterpret_cast<const int*>(stage)[e];
+        return make_double2((double)(int)(short)(r & 0xffff), (double)(r >> 16));
+    } else {
+        return reinterpret_cast<const double2*>(stage)[e];
+    }
+}
+
 template <int LOGN, bool STAGED, bool I16>
 __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
 {
@@ -377,182 +496,223 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
     constexpr int N = FS::N, T = FS::T;
     constexpr int SW = STAGED ? 1 : RX_SMAX;  // register window (symbols)
     extern __shared__ double2 smem[];
-    const int S = a.S, D = a.D, P = a.P;
+    const int S0 = a.S, P0 = a.P;
     double2* bufA = smem;                   // FFT ping-pong images
     double2* bufB = bufA + N;
     double2* lds_tw = bufB + FS::PADN;      // TwLds::SIZE
     double2* pil = lds_tw + TwLds<LOGN>::SIZE;  // S*P raw pilots
-    double2* gain = pil + S * P;            // S*P equaliser gains
-    double* red = reinterpret_cast<double*>(gain + S * P);
+    double2* gain = pil + S0 * P0;          // S*P equaliser gains
+    double* red = reinterpret_cast<double*>(gain + S0 * P0);
     uint8_t* dec = reinterpret_cast<uint8_t*>(bufA);  // aliases the FFT images after the transforms
 
-    const int t = threadIdx.x;
-    const long f = blockIdx.x;
+    const int t0 = threadIdx.x;
     const int L = N + a.cp;
-    const long x0 = f * a.frame_stride + a.cp;  // CP strip (Frame.hpp:278-279)
+    const long fstep = gridDim.x;
 
-    // table loads first, then symbol 0: every prologue wait below is a
-    // counted vmcnt that leaves the symbol prefetch in flight
+    // table loads first, then symbol 0 of the first frame: every prologue wait
+    // below is a counted vmcnt that leaves the symbol prefetch in flight
     constexpr bool kTwSplit = T >= TwLds<LOGN>::SIZE;
     TwPiece<LOGN> twp{};
     if constexpr (kTwSplit)
-        twp = tw_fetch<LOGN>(a.tab.tw, t);
+        twp = tw_fetch<LOGN>(a.tab.tw, t0);
     else
-        load_twiddles<LOGN>(a.tab.tw, lds_tw, t, T);
-    // data carrier d = t + T*i: swizzled LDS slot of its FFT bin (low 16 bits)
+        load_twiddles<LOGN>(a.tab.tw, lds_tw, t0, T);
+    // data carrier d = t0 + T*i: swizzled LDS slot of its FFT bin (low 16 bits)
     // | pilot slot (high 16); host tables are zero-padded, so no guards here
     int pk[RX_DPT];
 #pragma unroll
-    for (int i = 0; i < RX_DPT; ++i) pk[i] = a.tab.rx_pack[t + T * i];
-    const int pbin = a.tab.pilot_swz[t];
+    for (int i = 0; i < RX_DPT; ++i) pk[i] = a.tab.rx_pack[t0 + T * i];
+    const int pbin = a.tab.pilot_swz[t0];
+    long f = blockIdx.x;
     SymbolRegs<LOGN, I16> pf;
-    pf.load(a, x0, t);
+    dma_symbol<LOGN, I16>(a, f * a.frame_stride + a.cp, bufB, t0);  // grid <= nframes
     if constexpr (kTwSplit) tw_store<LOGN>(twp, lds_tw);
     lds_barrier();  // twiddle table visible: fft_pp reads a pass's twiddles before its barrier
 
-    double2 y[SW][RX_DPT];
-    double2* first = bufA;
-    double2* second = bufB;
+    unsigned long long errs = 0;
+
+    // Persistent over frames (grid <= 2 workgroups per CU): the next frame's
+    // symbol 0 is fetched (LDS-DMA into bufB) while this frame's epilogue
+    // runs, so HBM reads do not stop between frames, and the tables are
+    // loaded once per workgroup.
 #pragma unroll 1
-    for (int s = 0; s < S; ++s) {
-        double2 v[8];
+    for (; f < a.nframes; f += fstep) {
+        // Opaque per-frame copies of the thread index, the carrier tables and
+        // the geometry: everything derived from them is recomputed per frame
+        // instead of being hoisted out of the frame loop and held live beside
+        // the register window (which spills).
+        int t;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(t0));
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = pf.get(i);
-        if (s + 1 < S) pf.load(a, x0 + (long)(s + 1) * L, t);
-        // opaque copy of t: the per-pass LDS addresses are recomputed each
-        // symbol instead of being hoisted out of the loop and held live
-        // beside the register window
-        int tl;
-        asm volatile("v_mov_b32 %0, %1" : "=v"(tl) : "v"(t));
-        double2* res = fft_pp<LOGN, -1>(v, tl, lds_tw, first, second);
-        first = res == bufA ? bufB : bufA;
-        second = res;
-        if (t < P) pil[s * P + t] = res[pbin];
-        if constexpr (STAGED) {
+        for (int i = 0; i < RX_DPT; ++i) asm volatile("" : "+v"(pk[i]));
+        int S = a.S, D = a.D, P = a.P;
+        asm volatile("" : "+s"(S), "+s"(D), "+s"(P));
+        const long x0 = f * a.frame_stride + a.cp;  // CP strip (Frame.hpp:278-279)
+        const int m = 1 << (a.k / 2);
+        const double s1 = a.k == 1 ? 0.0 : 1.0 / (2.0 / (m - 1));
+        const bool whole_frame_dec = (long)S * D <= (long)FS::PADN * 16;
+        const long bpf = a.bytes_per_frame;
+        // word-wise packing: k in {1,2,4,8}, whole words, 4-byte aligned outputs
+        const bool by_word = (a.k == 1 || a.k == 2 || a.k == 4 || a.k == 8) && (bpf & 3) == 0 &&
+                             ((uintptr_t)a.bytes & 3) == 0 && ((uintptr_t)a.ref & 3) == 0;
+        double2 y[SW][RX_DPT];
+        // symbol 0 is read from bufB, so pass 0 writes bufA (free: the
+        // previous epilogue ended with a barrier)
+        double2* first = bufA;
+        double2* second = bufB;
+#pragma unroll 1
+        for (int s = 0; s < S; ++s) {
+            double2 v[8];
+            if (s == 0) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of symbol 0 landed
 #pragma unroll
-            for (int i = 0; i < RX_DPT; ++i) {
-                const int d = t + T * i;
-                if (d < D) a.ystage[(f * S + s) * D + d] = res[pk[i] & 0xffff];
+                for (int i = 0; i < 8; ++i) v[i] = stage_get<LOGN, I16>(bufB, t + T * i);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v[i] = pf.get(i);
             }
-        } else {
-            switch (s) {
+            if (s + 1 < S) pf.load(a, x0 + (long)(s + 1) * L, t);
+            // opaque copy of t: the per-pass LDS addresses are recomputed each
+            // symbol instead of being hoisted out of the loop and held live
+            // beside the register window
+            int tl;
+            asm volatile("v_mov_b32 %0, %1" : "=v"(tl) : "v"(t));
+            double2* res = fft_pp<LOGN, -1>(v, tl, lds_tw, first, second);
+            first = res == bufA ? bufB : bufA;
+            second = res;
+            if (t < P) pil[s * P + t] = res[pbin];
+            if constexpr (STAGED) {
+#pragma unroll
+                for (int i = 0; i < RX_DPT; ++i) {
+                    const int d = t + T * i;
+                    if (d < D) a.ystage[(f * S + s) * D + d] = res[pk[i] & 0xffff];
+                }
+            } else {
+                switch (s) {
 #define OFDM_RX_PUT(W)                                                                    \
     case W:                                                                               \
         if constexpr (W < SW) {                                                           \
             _Pragma("unroll") for (int i = 0; i < RX_DPT; ++i) y[W][i] = res[pk[i] & 0xffff]; \
         }                                                                                 \
         break;
-                OFDM_RX_PUT(0) OFDM_RX_PUT(1) OFDM_RX_PUT(2) OFDM_RX_PUT(3)
-                OFDM_RX_PUT(4) OFDM_RX_PUT(5) OFDM_RX_PUT(6) OFDM_RX_PUT(7)
+                    OFDM_RX_PUT(0) OFDM_RX_PUT(1) OFDM_RX_PUT(2) OFDM_RX_PUT(3)
+                    OFDM_RX_PUT(4) OFDM_RX_PUT(5) OFDM_RX_PUT(6) OFDM_RX_PUT(7)
 #undef OFDM_RX_PUT
-                default: break;
-            }
-        }
-    }
-    lds_barrier();  // pilots of the last symbol visible
-
-    // phys_pilot_ampl = sum |pilot| / (P*S*pilot_ampl)   (Frame.cpp:76-80)
-    double acc = 0.0;
-    for (int i = t; i < S * P; i += T) acc += hypot(pil[i].x, pil[i].y);
-    acc = block_sum<T>(acc, red);
-    const double phys = acc / ((double)(P * S) * a.pilot_ampl);
-
-    // out = (F/phys) / ((F[s,p]/phys) / (F[0,p]/phys)) = F * gain[s][j]   (Frame.cpp:82-93)
-    for (int i = t; i < S * P; i += T) {
-        const int j = i % P;
-        const double2 c0 = make_double2(pil[j].x / phys, pil[j].y / phys);
-        const double2 cs = make_double2(pil[i].x / phys, pil[i].y / phys);
-        const double2 coef = cdiv_exact(cs, c0);
-        const double2 g = cdiv_exact(make_double2(1.0, 0.0), coef);
-        gain[i] = make_double2(g.x / phys, g.y / phys);
-    }
-    __syncthreads();
-
-    const int m = 1 << (a.k / 2);
-    const double s1 = a.k == 1 ? 0.0 : 1.0 / (2.0 / (m - 1));
-    const double2* chan = a.chan ? a.chan + f * a.chan_stride : nullptr;
-    const bool whole_frame_dec = (long)S * D <= (long)FS::PADN * 16;
-
-    auto emit = [&](int s, int i, double2 yv) {
-        const int d = t + T * i;
-        double2 o = cmul_exact(yv, gain[s * P + (pk[i] >> 16)]);
-        if (chan) o = cdiv_exact(o, chan[d]);
-        if (a.constell) store_nt(a.constell + (f * S + s) * D + d, o);
-        dec[whole_frame_dec ? s * D + d : d] = (uint8_t)decide(o, a.k, s1, m);
-    };
-
-    const long bpf = a.bytes_per_frame;
-    unsigned long long errs = 0;
-    auto pack = [&](long jb0, long jb1, long dbase) {
-        for (long jb = jb0 + t; jb < jb1; jb += T) {
-            int byte = 0;
-            if (a.k == 1 || a.k == 2 || a.k == 4 || a.k == 8) {
-                const int per = 8 / a.k;
-                const long p0 = (jb - jb0) * per + dbase;
-                for (int r = 0; r < per; ++r) byte = (byte << a.k) | dec[p0 + r];
-            } else {
-                for (int b = 0; b < 8; ++b) {
-                    const long bit = (jb - jb0) * 8 + b;
-                    const long g = bit / a.k + dbase;
-                    const int within = (int)(bit % a.k);
-                    byte = (byte << 1) | ((dec[g] >> (a.k - 1 - within)) & 1);
+                    default: break;
                 }
             }
-            if (a.bytes) a.bytes[f * bpf + jb] = (uint8_t)byte;
-            if (a.ref) errs += __popc((unsigned)(byte ^ a.ref[f * bpf + jb]));
         }
-    };
+        lds_barrier();  // pilots of the last symbol visible; every thread is done reading bufB
+        if (f + fstep < a.nframes) dma_symbol<LOGN, I16>(a, (f + fstep) * a.frame_stride + a.cp, bufB, t);
 
-    // word-wise packing: k in {1,2,4,8}, whole words, 4-byte aligned outputs
-    const bool by_word = (a.k == 1 || a.k == 2 || a.k == 4 || a.k == 8) && (bpf & 3) == 0 &&
-                         ((uintptr_t)a.bytes & 3) == 0 && ((uintptr_t)a.ref & 3) == 0;
-    auto pack_words = [&]() {
-        const int per_word = 32 / a.k;  // decisions per output word
-        for (long w = t; w < bpf / 4; w += T) {
-            const uint8_t* dw = dec + w * per_word;
-            uint32_t word;
-            switch (a.k) {
-                case 1: word = pack_word<1>(dw); break;
-                case 2: word = pack_word<2>(dw); break;
-                case 4: word = pack_word<4>(dw); break;
-                default: word = pack_word<8>(dw); break;
+        // phys_pilot_ampl = sum |pilot| / (P*S*pilot_ampl)   (Frame.cpp:76-80)
+        double acc = 0.0;
+        for (int i = t; i < S * P; i += T) acc += hypot(pil[i].x, pil[i].y);
+        acc = block_sum_lds<T>(acc, red);
+        const double phys = acc / ((double)(P * S) * a.pilot_ampl);
+
+        // out = (F/phys) / ((F[s,p]/phys) / (F[0,p]/phys)) = F * gain[s][j]   (Frame.cpp:82-93)
+        for (int i = t; i < S * P; i += T) {
+            const int j = i % P;
+            const double2 c0 = make_double2(pil[j].x / phys, pil[j].y / phys);
+            const double2 cs = make_double2(pil[i].x / phys, pil[i].y / phys);
+            const double2 coef = cdiv_exact(cs, c0);
+            const double2 g = cdiv_exact(make_double2(1.0, 0.0), coef);
+            gain[i] = make_double2(g.x / phys, g.y / phys);
+        }
+        lds_barrier();
+
+        const double2* chan = a.chan ? a.chan + f * a.chan_stride : nullptr;
+        auto emit = [&](int s, int i, double2 yv) {
+            // opaque: the per-point addresses are computed here, not hoisted
+            // out of the emit loop and held (32 of them) across it
+            int d = t + T * i, gi = s * P + (pk[i] >> 16);
+            asm volatile("" : "+v"(d), "+v"(gi));
+            double2 o = cmul_exact(yv, gain[gi]);
+            if (chan) o = cdiv_exact(o, chan[d]);
+            if (a.constell) store_nt(a.constell + (f * S + s) * D + d, o);
+            dec[whole_frame_dec ? s * D + d : d] = (uint8_t)decide(o, a.k, s1, m);
+        };
+
+        auto pack = [&](long jb0, long jb1, long dbase) {
+            for (long jb = jb0 + t; jb < jb1; jb += T) {
+                int byte = 0;
+                if (a.k == 1 || a.k == 2 || a.k == 4 || a.k == 8) {
+                    const int per = 8 / a.k;
+                    const long p0 = (jb - jb0) * per + dbase;
+                    for (int r = 0; r < per; ++r) byte = (byte << a.k) | dec[p0 + r];
+                } else {
+                    for (int b = 0; b < 8; ++b) {
+                        const long bit = (jb - jb0) * 8 + b;
+                        const long g = bit / a.k + dbase;
+                        const int within = (int)(bit % a.k);
+                        byte = (byte << 1) | ((dec[g] >> (a.k - 1 - within)) & 1);
+                    }
+                }
+                if (a.bytes) a.bytes[f * bpf + jb] = (uint8_t)byte;
+                if (a.ref) errs += __popc((unsigned)(byte ^ a.ref[f * bpf + jb]));
             }
-            if (a.bytes) reinterpret_cast<uint32_t*>(a.bytes + f * bpf)[w] = word;
-            if (a.ref) errs += __popc(word ^ reinterpret_cast<const uint32_t*>(a.ref + f * bpf)[w]);
-        }
-    };
+        };
 
-    if constexpr (!STAGED) {
-#pragma unroll
-        for (int w = 0; w < SW; ++w) {
-            if (w < S) {
+        auto pack_words = [&]() {
+            const int per_word = 32 / a.k;  // decisions per output word
+            for (long w = t; w < bpf / 4; w += T) {
+                const uint8_t* dw = dec + w * per_word;
+                uint32_t word;
+                switch (a.k) {
+                    case 1: word = pack_word<1>(dw); break;
+                    case 2: word = pack_word<2>(dw); break;
+                    case 4: word = pack_word<4>(dw); break;
+                    default: word = pack_word<8>(dw); break;
+                }
+                if (a.bytes) reinterpret_cast<uint32_t*>(a.bytes + f * bpf)[w] = word;
+                if (a.ref) errs += __popc(word ^ reinterpret_cast<const uint32_t*>(a.ref + f * bpf)[w]);
+            }
+        };
+
+        if constexpr (!STAGED) {
+            // one symbol per (non-unrolled) iteration: a case's register
+            // indices are compile-time, and the scheduler cannot interleave
+            // symbols (the next frame's symbol 0 is live in registers here)
+#pragma unroll 1
+            for (int w = 0; w < S; ++w) {
+                switch (w) {
+#define OFDM_RX_EMIT(W)                                                                   \
+    case W:                                                                               \
+        if constexpr (W < SW) {                                                           \
+            _Pragma("unroll") for (int i = 0; i < RX_DPT; ++i) if (t + T * i < D) emit(w, i, y[W][i]); \
+        }                                                                                 \
+        break;
+                    OFDM_RX_EMIT(0) OFDM_RX_EMIT(1) OFDM_RX_EMIT(2) OFDM_RX_EMIT(3)
+                    OFDM_RX_EMIT(4) OFDM_RX_EMIT(5) OFDM_RX_EMIT(6) OFDM_RX_EMIT(7)
+#undef OFDM_RX_EMIT
+                    default: break;
+                }
+            }
+            lds_barrier();
+            if (by_word)
+                pack_words();
+            else
+                pack(0, bpf, 0);
+        } else {
+            const long bps = (long)D * a.k / 8;  // bytes per symbol (host checks D*k % 8 == 0)
+            for (int s = 0; s < S; ++s) {
 #pragma unroll
                 for (int i = 0; i < RX_DPT; ++i)
-                    if (t + T * i < D) emit(w, i, y[w][i]);
+                    if (t + T * i < D) emit(s, i, a.ystage[(f * S + s) * D + t + T * i]);
+                lds_barrier();
+                if (!whole_frame_dec) {
+                    pack(s * bps, (s + 1) * bps, 0);
+                    lds_barrier();
+                }
             }
+            if (whole_frame_dec) pack(0, bpf, 0);
         }
-        __syncthreads();
-        if (by_word)
-            pack_words();
-        else
-            pack(0, bpf, 0);
-    } else {
-        const long bps = (long)D * a.k / 8;  // bytes per symbol (host checks D*k % 8 == 0)
-        for (int s = 0; s < S; ++s) {
-#pragma unroll
-            for (int i = 0; i < RX_DPT; ++i)
-                if (t + T * i < D) emit(s, i, a.ystage[(f * S + s) * D + t + T * i]);
-            __syncthreads();
-            if (!whole_frame_dec) {
-                pack(s * bps, (s + 1) * bps, 0);
-                __syncthreads();
-            }
-        }
-        if (whole_frame_dec) pack(0, bpf, 0);
+        lds_barrier();  // dec / pil / gain / red are rewritten by the next frame
     }
     if (a.bit_errors) {
         errs = block_sum_u64<T>(errs, red);
-        if (t == 0 && errs) atomicAdd(a.bit_errors, errs);
+        if (t0 == 0 && errs) atomicAdd(a.bit_errors, errs);
     }
 }
 
@@ -633,43 +793,63 @@ __global__ void f64_to_i16_kernel(const double2* __restrict__ in, long n, double
 }
 
 // ------------------------------------------------------------------ launchers
-template <int LOGN, bool POINTS>
+template <int LOGN, bool POINTS, bool NOISE, bool I16>
 static hipError_t tx_launch_n(const TxArgs& a, hipStream_t st)
 {
     using FS = FftShape<LOGN>;
-    const size_t shm = sizeof(double2) * (FS::PADN + TwLds<LOGN>::SIZE + 256) + FS::N;  // + table + payload
+    const size_t shm = sizeof(double2) * (FS::PADN + TwLds<LOGN>::SIZE + TX_LDS_ZERO + 1) + FS::N;  // + points + payload
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)tx_kernel<LOGN, POINTS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)shm);
+        (void)hipFuncSetAttribute((const void*)tx_kernel<LOGN, POINTS, NOISE, I16>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
         attr = true;
     }
     const long nsym = a.nframes * a.S;
     if (nsym <= 0) return hipSuccess;
     // persistent grid: enough workgroups to fill every CU several times over
     const long grid = nsym < TX_MAX_GRID ? nsym : TX_MAX_GRID;
-    hipLaunchKernelGGL((tx_kernel<LOGN, POINTS>), dim3((unsigned)grid), dim3(FS::T), shm, st, a);
+    hipLaunchKernelGGL((tx_kernel<LOGN, POINTS, NOISE, I16>), dim3((unsigned)grid), dim3(FS::T), shm, st, a);
     return hipGetLastError();
 }
 
-template <bool POINTS>
-static hipError_t launch_tx_p(int logn, const TxArgs& a, hipStream_t st)
+template <int LOGN>
+static hipError_t tx_launch_modes(const TxArgs& a, hipStream_t st)
 {
-    switch (logn) {
-        case 6: return tx_launch_n<6, POINTS>(a, st);
-        case 7: return tx_launch_n<7, POINTS>(a, st);
-        case 8: return tx_launch_n<8, POINTS>(a, st);
-        case 9: return tx_launch_n<9, POINTS>(a, st);
-        case 10: return tx_launch_n<10, POINTS>(a, st);
-        case 11: return tx_launch_n<11, POINTS>(a, st);
-        case 12: return tx_launch_n<12, POINTS>(a, st);
-        default: return hipErrorInvalidValue;
+    const bool noise = a.noise_scale > 0.0, i16 = a.iq16 != nullptr;
+    if (a.points) {
+        if (noise) return i16 ? tx_launch_n<LOGN, true, true, true>(a, st) : tx_launch_n<LOGN, true, true, false>(a, st);
+        return i16 ? tx_launch_n<LOGN, true, false, true>(a, st) : tx_launch_n<LOGN, true, false, false>(a, st);
     }
+    if (noise) return i16 ? tx_launch_n<LOGN, false, true, true>(a, st) : tx_launch_n<LOGN, false, true, false>(a, st);
+    return i16 ? tx_launch_n<LOGN, false, false, true>(a, st) : tx_launch_n<LOGN, false, false, false>(a, st);
 }
 
 hipError_t launch_tx(int logn, const TxArgs& a, hipStream_t st)
 {
-    return a.points ? launch_tx_p<true>(logn, a, st) : launch_tx_p<false>(logn, a, st);
+    switch (logn) {
+        case 6: return tx_launch_modes<6>(a, st);
+        case 7: return tx_launch_modes<7>(a, st);
+        case 8: return tx_launch_modes<8>(a, st);
+        case 9: return tx_launch_modes<9>(a, st);
+        case 10: return tx_launch_modes<10>(a, st);
+        case 11: return tx_launch_modes<11>(a, st);
+        case 12: return tx_launch_modes<12>(a, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+// Compute units of the current device (cached per device).
+static int num_cus()
+{
+    static int cache[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    if (!cache[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cache[dev] = n;
+    }
+    return cache[dev];
 }
 
 template <int LOGN>
@@ -692,7 +872,10 @@ static hipError_t rx_launch_n(const RxArgs& a, hipStream_t st)
         attr = 160 * 1024;
     }
     if (a.nframes <= 0) return hipSuccess;
-    hipLaunchKernelGGL((rx_kernel<LOGN, STAGED, I16>), dim3((unsigned)a.nframes), dim3(FS::T), shm, st, a);
+    // persistent: at most RX_WG_PER_CU workgroups per CU (the register window's occupancy)
+    const long cap = (long)RX_WG_PER_CU * num_cus();
+    const long grid = a.nframes < cap ? a.nframes : cap;
+    hipLaunchKernelGGL((rx_kernel<LOGN, STAGED, I16>), dim3((unsigned)grid), dim3(FS::T), shm, st, a);
     return hipGetLastError();
 }
 
