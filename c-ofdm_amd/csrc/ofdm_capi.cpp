@@ -1193,11 +1193,89 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     const size_t nout = std::min(frames.size(), max_frames);
     if (nout == 0) return OFDM_OK;
 
-    // located frames -> batch -> main.cpp:60-80 chain + demod, in bounded batches
+    // located frames -> main.cpp:60-80 chain + demod
     if ((rc = grow(c, c->s_pbs, nout * sizeof(long)))) return rc;
     long* d_pbs = static_cast<long*>(c->s_pbs.p);
     HIP_TRY(hipMemcpyAsync(d_pbs, frames.data(), nout * sizeof(long), hipMemcpyHostToDevice, st));
     if (pb_out) HIP_TRY(hipMemcpyAsync(pb_out, d_pbs, nout * sizeof(long), hipMemcpyDeviceToDevice, st));
+
+    // Fused path: three kernels read each frame from the stream in place
+    // (pilot_freq_sinh; the other sync stages' parameters + chan_char_lq;
+    // rx with the corrections applied on load), no frame copy, no corrected
+    // copy. Needs the register-window rx and a pilot_freq_sinh plan.
+    ofdm_ctx::CfoPlan* pl = nullptr;
+    const bool fused = c->S <= ofdm::RX_SMAX && c->D <= ofdm::RX_DPT * (c->N / 8) && c->P <= c->N / 8 &&
+                       c->npr + c->S <= 64 && cfo_plan(c, c->npr, &pl) == OFDM_OK;
+    if (fused) {
+        const size_t per = (size_t)c->D * sizeof(double2) + (size_t)c->S * 4 * sizeof(double) + sizeof(double);
+        const size_t bmax = std::max<size_t>(1, ((size_t)256 << 20) / per);
+        const size_t nb0 = std::min(nout, bmax);
+        if ((rc = grow(c, c->s_chan, nb0 * per))) return rc;
+        double2* chan = static_cast<double2*>(c->s_chan.p);
+        double* corr = reinterpret_cast<double*>(chan + nb0 * c->D);
+        double* cfo_tmp = corr + nb0 * c->S * 4;
+        const long npts = (long)c->D * c->S;
+        for (size_t f0 = 0; f0 < nout; f0 += nb0) {
+            const size_t nb = std::min(nb0, nout - f0);
+            double* cfo = cfo_out ? cfo_out + f0 : cfo_tmp;
+            ofdm::CfoArgs ca{};
+            ca.x = reinterpret_cast<const double2*>(iq);
+            ca.x16 = reinterpret_cast<const short2*>(iq16);
+            ca.starts = d_pbs + f0;
+            ca.nframes = (long)nb;
+            ca.tw_sub = pl->tw_sub;
+            ca.tw_full = pl->tw_full;
+            ca.borders = pl->borders;
+            ca.P = c->P;
+            ca.cfo_out = cfo;
+            e = ofdm::launch_cfo(pl->logm, pl->g, ca, st);
+            if (e != hipSuccess) return hip_fail(e, "stream cfo launch");
+            ofdm::StreamParamsArgs sa{};
+            sa.tab = c->tables(true);
+            sa.iq = reinterpret_cast<const double2*>(iq);
+            sa.iq16 = reinterpret_cast<const short2*>(iq16);
+            sa.starts = d_pbs + f0;
+            sa.nframes = (long)nb;
+            sa.cfo = cfo;
+            sa.pre = c->d_preamble;
+            sa.mod_pre = c->d_modpre;
+            sa.chan_out = chan;
+            sa.corr_out = corr;
+            sa.npr = c->npr;
+            sa.S = c->S;
+            sa.D = c->D;
+            sa.P = c->P;
+            sa.cp = c->cp;
+            sa.pilot_ampl = (double)c->p.pilot_ampl / 1000;
+            e = ofdm::launch_stream_params(c->logn, sa, st);
+            if (e != hipSuccess) return hip_fail(e, "stream params launch");
+            ofdm::RxArgs ra{};
+            ra.tab = c->tables(false);
+            ra.iq = reinterpret_cast<const double2*>(iq);
+            ra.iq16 = reinterpret_cast<const short2*>(iq16);
+            ra.nframes = (long)nb;
+            ra.starts = d_pbs + f0;
+            ra.start_off = pre + c->cp;
+            ra.corr = corr;
+            ra.chan = chan;
+            ra.chan_stride = c->D;
+            ra.constell = constell_out ? reinterpret_cast<double2*>(constell_out) + f0 * npts : nullptr;
+            ra.bytes = bytes_out ? bytes_out + f0 * c->geo.bytes_per_frame : nullptr;
+            ra.S = c->S;
+            ra.D = c->D;
+            ra.P = c->P;
+            ra.seg = c->seg;
+            ra.cp = c->cp;
+            ra.k = c->k;
+            ra.bytes_per_frame = c->geo.bytes_per_frame;
+            ra.pilot_ampl = (double)c->p.pilot_ampl / 1000;
+            e = ofdm::launch_rx(c->logn, ra, st, nullptr);
+            if (e != hipSuccess) return hip_fail(e, "stream rx launch");
+        }
+        return OFDM_OK;
+    }
+
+    // Fallback: gather each frame into a batch, then the staged sync chain + demod
     const size_t fb = (size_t)span * sizeof(double2);
     const size_t bmax = std::max<size_t>(1, std::min<size_t>(65535, ((size_t)256 << 20) / fb));
     const size_t nb0 = std::min(nout, bmax);

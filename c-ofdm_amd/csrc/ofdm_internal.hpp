@@ -54,6 +54,13 @@ struct RxArgs {
     const uint8_t* ref;         // nullable
     unsigned long long* bit_errors;  // nullable
     double2* ystage;            // staged variant only: nframes*S*D scratch
+    // stream mode (fused stream decode): frame f's message body starts at
+    // starts[f] + start_off, and message symbol s is multiplied by the phase
+    // ramp e^{i(A + B m)} of corr[(f*S + s)*4 ..] = {A, B, cos(B*T), sin(B*T)}
+    // (freq_shift + cp_freq_sinh + pr_phase_sinh, ofdm_sync.hip stream_params_kernel)
+    const long* starts;         // nullable
+    long start_off;
+    const double* corr;
     int S, D, P, seg, cp, k;
     long bytes_per_frame;
     double pilot_ampl;
@@ -75,8 +82,8 @@ constexpr int RX_SMAX = 8;
 // LDS slot of FFT element e (ofdm_fft.hpp lds_swz), for host-built tables
 inline int lds_swz_host(int e) { return e ^ ((e >> 3) & 7); }
 constexpr int RX_DPT = 4;
-// rx: persistent workgroups per CU (2 x 4 waves: the register window's occupancy)
-constexpr int RX_WG_PER_CU = 2;
+// rx: persistent resident waves per CU (2 per SIMD: the register window's occupancy)
+constexpr int RX_WAVES_PER_CU = 8;
 // tx per-bin code: bits 0-12 data index d, bits 13-20 mask applied to its
 // k-bit payload symbol (0xff data, 0 otherwise), bits 21-29 base entry of the
 // tx kernel's LDS point table (0 for data; TX_LDS_PILOT / TX_LDS_ZERO hold the

@@ -489,7 +489,7 @@ __device__ __forceinline__ double2 stage_get(const void* stage, int e)
     }
 }
 
-template <int LOGN, bool STAGED, bool I16>
+template <int LOGN, bool STAGED, bool I16, bool SYNC>
 __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
 {
     using FS = FftShape<LOGN>;
@@ -525,7 +525,9 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
     const int pbin = a.tab.pilot_swz[t0];
     long f = blockIdx.x;
     SymbolRegs<LOGN, I16> pf;
-    dma_symbol<LOGN, I16>(a, f * a.frame_stride + a.cp, bufB, t0);  // grid <= nframes
+    // sample offset of frame g's first message body (CP strip, Frame.hpp:278-279)
+    auto body0 = [&](long g) { return SYNC ? a.starts[g] + a.start_off : g * a.frame_stride + a.cp; };
+    dma_symbol<LOGN, I16>(a, body0(f), bufB, t0);  // grid <= nframes
     if constexpr (kTwSplit) tw_store<LOGN>(twp, lds_tw);
     lds_barrier();  // twiddle table visible: fft_pp reads a pass's twiddles before its barrier
 
@@ -547,7 +549,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
         for (int i = 0; i < RX_DPT; ++i) asm volatile("" : "+v"(pk[i]));
         int S = a.S, D = a.D, P = a.P;
         asm volatile("" : "+s"(S), "+s"(D), "+s"(P));
-        const long x0 = f * a.frame_stride + a.cp;  // CP strip (Frame.hpp:278-279)
+        const long x0 = body0(f);
         const int m = 1 << (a.k / 2);
         const double s1 = a.k == 1 ? 0.0 : 1.0 / (2.0 / (m - 1));
         const bool whole_frame_dec = (long)S * D <= (long)FS::PADN * 16;
@@ -572,6 +574,20 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
                 for (int i = 0; i < 8; ++i) v[i] = pf.get(i);
             }
             if (s + 1 < S) pf.load(a, x0 + (long)(s + 1) * L, t);
+            if constexpr (SYNC) {
+                // sample m = t + T*i of the body: *= e^{i(A + B m)}, by a
+                // running product from e^{i(A + B t)} in steps of e^{i B T}
+                const double* cr = a.corr + (f * S + s) * 4;
+                const double2 w = make_double2(cr[2], cr[3]);
+                double sn, cs;
+                sincos(cr[0] + cr[1] * (double)t, &sn, &cs);
+                double2 c = make_double2(cs, sn);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    v[i] = cmul(v[i], c);
+                    if (i < 7) c = cmul(c, w);
+                }
+            }
             // opaque copy of t: the per-pass LDS addresses are recomputed each
             // symbol instead of being hoisted out of the loop and held live
             // beside the register window
@@ -603,7 +619,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
             }
         }
         lds_barrier();  // pilots of the last symbol visible; every thread is done reading bufB
-        if (f + fstep < a.nframes) dma_symbol<LOGN, I16>(a, (f + fstep) * a.frame_stride + a.cp, bufB, t);
+        if (f + fstep < a.nframes) dma_symbol<LOGN, I16>(a, body0(f + fstep), bufB, t);
 
         // phys_pilot_ampl = sum |pilot| / (P*S*pilot_ampl)   (Frame.cpp:76-80)
         double acc = 0.0;
@@ -859,7 +875,7 @@ static size_t rx_shm(const RxArgs& a)
     return sizeof(double2) * (FS::N + FS::PADN + TwLds<LOGN>::SIZE + 2 * (size_t)a.S * a.P) + 32 * sizeof(double);
 }
 
-template <int LOGN, bool STAGED, bool I16>
+template <int LOGN, bool STAGED, bool I16, bool SYNC>
 static hipError_t rx_launch_n(const RxArgs& a, hipStream_t st)
 {
     using FS = FftShape<LOGN>;
@@ -867,15 +883,18 @@ static hipError_t rx_launch_n(const RxArgs& a, hipStream_t st)
     if (shm > 160 * 1024) return hipErrorInvalidValue;
     static int attr = 0;
     if ((size_t)attr < shm) {
-        (void)hipFuncSetAttribute((const void*)rx_kernel<LOGN, STAGED, I16>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024);
+        (void)hipFuncSetAttribute((const void*)rx_kernel<LOGN, STAGED, I16, SYNC>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = 160 * 1024;
     }
     if (a.nframes <= 0) return hipSuccess;
-    // persistent: at most RX_WG_PER_CU workgroups per CU (the register window's occupancy)
-    const long cap = (long)RX_WG_PER_CU * num_cus();
+    // persistent: RX_WAVES_PER_CU resident waves per CU (the register
+    // window's occupancy: 2 per SIMD), as far as LDS allows
+    const long per_cu_w = RX_WAVES_PER_CU / (FS::T >= 64 ? FS::T / 64 : 1);
+    const long per_cu_l = (long)(160 * 1024) / (long)shm;
+    const long cap = (per_cu_w < per_cu_l ? per_cu_w : per_cu_l) * num_cus();
     const long grid = a.nframes < cap ? a.nframes : cap;
-    hipLaunchKernelGGL((rx_kernel<LOGN, STAGED, I16>), dim3((unsigned)grid), dim3(FS::T), shm, st, a);
+    hipLaunchKernelGGL((rx_kernel<LOGN, STAGED, I16, SYNC>), dim3((unsigned)grid), dim3(FS::T), shm, st, a);
     return hipGetLastError();
 }
 
@@ -887,8 +906,13 @@ static hipError_t rx_dispatch(const RxArgs& a, hipStream_t st, bool* staged)
     if (staged) *staged = !fits;
     if (a.P > FS::T) return hipErrorInvalidValue;
     if (!fits && a.ystage == nullptr) return hipErrorInvalidValue;
-    if (a.iq16) return fits ? rx_launch_n<LOGN, false, true>(a, st) : rx_launch_n<LOGN, true, true>(a, st);
-    return fits ? rx_launch_n<LOGN, false, false>(a, st) : rx_launch_n<LOGN, true, false>(a, st);
+    if (a.starts) {  // stream mode: register window only
+        if (!fits || !a.corr) return hipErrorInvalidValue;
+        return a.iq16 ? rx_launch_n<LOGN, false, true, true>(a, st) : rx_launch_n<LOGN, false, false, true>(a, st);
+    }
+    if (a.iq16)
+        return fits ? rx_launch_n<LOGN, false, true, false>(a, st) : rx_launch_n<LOGN, true, true, false>(a, st);
+    return fits ? rx_launch_n<LOGN, false, false, false>(a, st) : rx_launch_n<LOGN, true, false, false>(a, st);
 }
 
 hipError_t launch_rx(int logn, const RxArgs& a, hipStream_t st, bool* staged)

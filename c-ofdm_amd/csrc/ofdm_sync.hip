@@ -21,6 +21,7 @@
 // recurrence and its exact j = 0..L-1 accumulation order (no FMA), so its
 // threshold decisions are bit-identical.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <climits>
 #include <cstdint>
 
@@ -292,11 +293,19 @@ __global__ void __launch_bounds__(G * (1 << LOGM) / 8) cfo_kernel(CfoArgs a)
     int* wsum = reinterpret_cast<int*>(amp + S);          // per-window argmax
     const int tid = threadIdx.x, g = tid / T, t = tid - g * T;
     const long f = blockIdx.x;
-    const double2* x = a.x + f * a.frame_stride;
+    const long x0 = a.starts ? a.starts[f] : f * a.frame_stride;
     load_twiddles<LOGM>(a.tw_sub, lds_tw, tid, NT);
     double2 v[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = x[(long)G * (t + T * i) + g];  // decimated input x[G*n + g]
+    for (int i = 0; i < 8; ++i) {  // decimated input x[G*n + g]
+        const long j = x0 + (long)G * (t + T * i) + g;
+        if (a.x16) {
+            const short2 w = a.x16[j];
+            v[i] = make_double2((double)w.x, (double)w.y);
+        } else {
+            v[i] = a.x[j];
+        }
+    }
     __syncthreads();
     fft_block<LOGM, -1>(v, t, lds_tw, fftb + g * M);
     // X[k + M*r] = sum_q W_S^{q k} W_G^{q r} F_q[k]; amp stored fftshifted:
@@ -605,6 +614,222 @@ hipError_t launch_chan(int logn, const ChanArgs& a, hipStream_t st)
         case 10: return chan_launch_n<10>(a, st);
         case 11: return chan_launch_n<11>(a, st);
         case 12: return chan_launch_n<12>(a, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+// ========================================================================
+// Fused stream decode, stage 2: main.cpp:61-65 on a located frame, read
+// straight from the stream (rx.cpp:185-189 copies the frame out first; here
+// nothing is copied and nothing corrected is written back).
+//   freq_shift     x[n] *= e^{-2 pi i cfo n}                (Frame.hpp:340-348)
+//   cp_freq_sinh   phi_q = arg sum_{j<cp} conj(y[qL+j]) y[qL+j+N] of the
+//                  shifted y; sample (q, j) *= e^{-i (psi_q L + phi_q j)/N},
+//                  psi_q = sum_{r<q} phi_r                  (Frame.hpp:238-263)
+//   pr_phase_sinh  phi_pr = arg sum_{i<pre} conj(pr_i) z_i; x *= e^{-i phi_pr}
+//                                                           (Frame.hpp:265-274)
+//   chan_char_lq   on the corrected preamble                (Frame.hpp:389-434)
+// conj(y_a) y_{a+N} = e^{-2 pi i cfo N} conj(x_a) x_{a+N}, so phi_q comes
+// from raw samples and one rotation of the sum. Every correction is one
+// phasor e^{i theta(q, j)}, theta linear in j within a symbol; the message
+// symbols' (A_s, B_s) are handed to the rx kernel (stream mode).
+// ========================================================================
+namespace {
+
+__device__ __forceinline__ double2 src_sample(const double2* iq, const short2* iq16, long j)
+{
+    if (iq16) {
+        const short2 w = iq16[j];
+        return make_double2((double)w.x, (double)w.y);
+    }
+    return iq[j];
+}
+
+}  // namespace
+
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamParamsArgs a)
+{
+    using FS = FftShape<LOGN>;
+    constexpr int N = FS::N, T = FS::T;
+    extern __shared__ double2 smem[];
+    double2* lds_tw = smem;
+    double2* fftb = lds_tw + TwLds<LOGN>::SIZE;   // N
+    double2* pil = fftb + N;                       // npr * P
+    double2* dat = pil + a.npr * a.P;              // D/2 raw bins of symbol 0
+    const int ndat = (a.D / 2 + 1) > (a.npr + a.S) * T ? (a.D / 2 + 1) : (a.npr + a.S) * T;
+    double* ph = reinterpret_cast<double*>(dat + ndat);
+    double2* red = reinterpret_cast<double2*>(ph + a.D / 2 + 2);  // 32 entries
+    double* phi = reinterpret_cast<double*>(red + 32);            // Q symbol phases
+    double* psi = phi + 64;                                       // Q prefix sums
+    double& phpr = psi[64];  // (dynamic LDS only: the 160 KiB attribute leaves no room for static)
+    const int t = threadIdx.x;
+    const long f = blockIdx.x;
+    const long x0 = a.starts[f];
+    const double cfo = a.cfo[f];
+    const int L = N + a.cp, half = a.D / 2, Q = a.npr + a.S;
+    const long pre = (long)L * a.npr;
+    load_twiddles<LOGN>(a.tab.tw, lds_tw, t, T);
+
+    // cp_freq_sinh phases of all Q symbols: per-thread partial sums of every
+    // symbol first (no barrier between symbols, so the loads of several
+    // symbols are in flight together), then one reduction per symbol
+    double2* part = dat;  // Q*T partials (dat is filled only later)
+    double rs, rc;
+    sincospi(-2.0 * cfo * (double)N, &rs, &rc);
+#pragma unroll 3
+    for (int q = 0; q < Q; ++q) {
+        double2 acc = make_double2(0.0, 0.0);
+#pragma unroll 2
+        for (int j = t; j < a.cp; j += T) {
+            const long i0 = x0 + (long)q * L + j;
+            acc = cadd(acc, cconj_mul(src_sample(a.iq, a.iq16, i0), src_sample(a.iq, a.iq16, i0 + N)));
+        }
+        part[q * T + t] = acc;
+    }
+    __syncthreads();
+    for (int q = t; q < Q; q += T) {
+        double2 acc = make_double2(0.0, 0.0);
+        for (int u = 0; u < T; ++u) acc = cadd(acc, part[q * T + u]);
+        const double2 r = cmul_exact(acc, make_double2(rc, rs));
+        phi[q] = atan2(r.y, r.x);
+    }
+    __syncthreads();
+    if (t == 0) {
+        double acc = 0.0;
+        for (int q = 0; q < Q; ++q) {
+            psi[q] = acc;
+            acc += phi[q];
+        }
+    }
+    __syncthreads();
+    // phase of form sample i = q*L + j before pr_phase_sinh
+    auto theta = [&](int q, int j) {
+        return -2.0 * M_PI * cfo * (double)((long)q * L + j) - (psi[q] * L + phi[q] * j) / N;
+    };
+    // pr_phase_sinh over the whole preamble form
+    {
+        double2 acc = make_double2(0.0, 0.0);
+#pragma unroll 4
+        for (long i = t; i < pre; i += T) {
+            const int q = (int)(i / L), j = (int)(i - (long)q * L);
+            double sn, cs;
+            sincos(theta(q, j), &sn, &cs);
+            const double2 z = cmul_exact(src_sample(a.iq, a.iq16, x0 + i), make_double2(cs, sn));
+            acc = cadd(acc, cconj_mul(a.pre[i], z));
+        }
+        acc = block_sum2<T>(acc, red);
+        if (t == 0) phpr = atan2(acc.y, acc.x);
+        __syncthreads();
+    }
+    const double phr = phpr;
+
+    // chan_char_lq: FFT_FORM::read of the corrected preamble symbols
+    for (int s = 0; s < a.npr; ++s) {
+        double2 v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int j = a.cp + t + T * i;
+            double sn, cs;
+            sincos(theta(s, j) - phr, &sn, &cs);
+            v[i] = cmul_exact(src_sample(a.iq, a.iq16, x0 + (long)s * L + j), make_double2(cs, sn));
+        }
+        __syncthreads();  // fftb free (previous symbol's reads done)
+        fft_block<LOGN, -1>(v, t, lds_tw, fftb);
+        for (int j = t; j < a.P; j += T) pil[s * a.P + j] = fftb[lds_swz(a.tab.pilot_bin[j])];
+        if (s == 0)
+            for (int i = t; i < half; i += T) dat[i] = fftb[lds_swz(a.tab.data_bin[i])];
+    }
+    __syncthreads();
+    double acc = 0.0;
+    for (int i = t; i < a.npr * a.P; i += T) acc += hypot(pil[i].x, pil[i].y);
+    acc = block_sum2<T>(make_double2(acc, 0.0), red).x;
+    const double phys = acc / ((double)(a.P * a.npr) * a.pilot_ampl);
+    for (int i = t; i < half; i += T) {
+        const int j = a.tab.data_slot[i];
+        const double2 p0 = make_double2(pil[j].x / phys, pil[j].y / phys);
+        const double2 coef = cdiv_exact(p0, p0);
+        const double2 fs = make_double2(dat[i].x / phys, dat[i].y / phys);
+        const double2 q = cdiv_exact(cdiv_exact(fs, coef), a.mod_pre[i]);
+        ph[i] = atan2(q.y, q.x);
+    }
+    __syncthreads();
+    if (t == 0) {  // one-pass unwrap against the already-adjusted previous value (Frame.hpp:407-414)
+        for (int i = 1; i < half; ++i) {
+            const double d = ph[i] - ph[i - 1];
+            if (d > M_PI)
+                ph[i] -= 2 * M_PI;
+            else if (d < -M_PI)
+                ph[i] += 2 * M_PI;
+        }
+    }
+    __syncthreads();
+    double sxy = 0.0, sy = 0.0;
+    for (int i = t; i < half; i += T) {
+        sxy += ph[i] * i;
+        sy += ph[i];
+    }
+    const double2 sums = block_sum2<T>(make_double2(sxy, sy), red + 16);
+    const double hn = (double)half;
+    const double sx = hn * (hn - 1) / 2, sx2 = (hn - 1) * hn * (2 * hn - 1) / 6;
+    const double b = (sums.x - sx * sums.y) / (sx2 - sx * sx);
+    const double aa = sums.y - b * sx;
+    double2* chan = a.chan_out + f * a.D;
+    for (int i = t; i < a.D; i += T) {
+        double th;
+        if (i < half)
+            th = add_rn(mul_rn(b, (double)i), aa);
+        else
+            th = add_rn(add_rn(mul_rn(-b, (double)a.D) / 2, mul_rn((double)(i - half), b)), aa);
+        double sn, cs;
+        sincos(th, &sn, &cs);
+        chan[i] = make_double2(cs, sn);
+    }
+    // message symbols: theta(m) = A_s + B_s m over the CP-stripped body
+    for (int s = t; s < a.S; s += T) {
+        const int q = a.npr + s;
+        const double A = theta(q, a.cp) - phr;
+        const double B = -2.0 * M_PI * cfo - phi[q] / N;
+        double sn, cs;
+        sincos(B * T, &sn, &cs);
+        double* o = a.corr_out + (f * a.S + s) * 4;
+        o[0] = A;
+        o[1] = B;
+        o[2] = cs;
+        o[3] = sn;
+    }
+}
+
+template <int LOGN>
+static hipError_t params_launch_n(const StreamParamsArgs& a, hipStream_t st)
+{
+    using FS = FftShape<LOGN>;
+    const size_t ndat = std::max<size_t>(a.D / 2 + 1, (size_t)(a.npr + a.S) * FS::T);  // bins, or CP partials
+    const size_t shm = sizeof(double2) * (TwLds<LOGN>::SIZE + FS::N + (size_t)a.npr * a.P + ndat) +
+                       sizeof(double) * (a.D / 2 + 2) + sizeof(double2) * 32 + sizeof(double) * 130;
+    if (shm > 160 * 1024) return hipErrorInvalidValue;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)stream_params_kernel<LOGN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL(stream_params_kernel<LOGN>, dim3((unsigned)a.nframes), dim3(FS::T), shm, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_stream_params(int logn, const StreamParamsArgs& a, hipStream_t st)
+{
+    if (a.nframes <= 0) return hipSuccess;
+    if (a.npr + a.S > 64) return hipErrorInvalidValue;
+    switch (logn) {
+        case 6: return params_launch_n<6>(a, st);
+        case 7: return params_launch_n<7>(a, st);
+        case 8: return params_launch_n<8>(a, st);
+        case 9: return params_launch_n<9>(a, st);
+        case 10: return params_launch_n<10>(a, st);
+        case 11: return params_launch_n<11>(a, st);
+        case 12: return params_launch_n<12>(a, st);
         default: return hipErrorInvalidValue;
     }
 }

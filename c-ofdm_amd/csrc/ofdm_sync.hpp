@@ -34,6 +34,8 @@ struct PreambleArgs {
 struct CfoArgs {
     const double2* x;
     long nframes, frame_stride;
+    const long* starts;      // nullable: frame f's form at x + starts[f] (stream decode)
+    const short2* x16;       // or: complex<int16> stream (with starts)
     const double2* tw_sub;   // M-point forward twiddles
     const double2* tw_full;  // S-point forward twiddles (G == 5)
     const int* borders;      // P + 2 window borders (Frame.hpp:311-321)
@@ -99,6 +101,29 @@ struct GatherArgs {
     long nframes, span;
     double2* dst;               // nframes * span
 };
+
+// Fused stream decode, stage 2 (after cfo_kernel): per located frame, the
+// cp_freq_sinh symbol phases, the pr_phase_sinh phase and chan_char_lq, all
+// from the raw stream samples (no corrected copy is written), plus for each
+// message symbol s the phase ramp theta(m) = A_s + B_s*m (m = sample of the
+// CP-stripped body) that freq_shift + cp_freq_sinh + pr_phase_sinh apply to
+// it, consumed by the rx kernel's stream mode.
+struct StreamParamsArgs {
+    DevTables tab;              // BPSK tables (the preamble is a BPSK symbol)
+    const double2* iq;          // stream
+    const short2* iq16;         // or complex<int16> stream
+    const long* starts;         // preamble start of each frame
+    long nframes;
+    const double* cfo;          // per frame (cfo_kernel)
+    const double2* pre;         // ofdm_preamble (npr*L samples)
+    const double2* mod_pre;     // D*npr BPSK points
+    double2* chan_out;          // nframes * D
+    double* corr_out;           // nframes * S * 4: A_s, B_s, cos(B_s*T), sin(B_s*T)
+    int npr, S, D, P, cp;
+    double pilot_ampl;
+};
+
+hipError_t launch_stream_params(int logn, const StreamParamsArgs& a, hipStream_t st);
 
 hipError_t launch_stream_walk(int logt, const WalkArgs& a, long nblocks, hipStream_t st);
 hipError_t launch_gather(const GatherArgs& a, hipStream_t st);
