@@ -11,6 +11,7 @@
 #include <complex>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <random>
@@ -1111,6 +1112,10 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     int* d_ids = d_nrec + nchunks;     // one re-walk chunk id (in the 64 B slack)
 
     ofdm::WalkArgs w{};
+    {
+        const char* ex = getenv("OFDM_WALK_EXACT");  // test hook: certified fast search off
+        w.exact_only = ex && ex[0] == '1';
+    }
     w.iq = reinterpret_cast<const double2*>(iq);
     w.iq16 = reinterpret_cast<const short2*>(iq16);
     w.n = nn;

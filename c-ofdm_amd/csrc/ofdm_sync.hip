@@ -866,11 +866,12 @@ __device__ __forceinline__ double2 stream_sample(const A& a, long j)
 
 // PREAMBLE_FORM::find_preamble from s: first lag with norm > 1 and
 // |sum_j x[s+i+j] c_j| / sqrt(norm) > level (Frame.cpp:338-378), INT_MAX if
-// none. The running energy is the reference's serial recurrence (+ new, then
-// - old, separately rounded) on per-sample energies computed in parallel;
-// lags are tested 256 at a time with an early exit.
-__device__ int walk_preamble(const WalkArgs& a, long s, double2* xs, const double2* c, double* E, double* normv,
-                             int* best, int t)
+// none. Exact form: the running energy is the reference's serial recurrence
+// (+ new, then - old, separately rounded) on per-sample energies computed in
+// parallel; lags are tested 256 at a time with an early exit. xs: C + L
+// samples, E: C + L energies, normv: C running energies (all LDS).
+__device__ int walk_preamble_exact(const WalkArgs& a, long s, double2* xs, const double2* c, double* E,
+                                   double* normv, int* best, int t)
 {
     const int L = a.L, C = a.cycles;
     for (int i = t; i < C + L; i += WALK_THREADS) {
@@ -909,6 +910,101 @@ __device__ int walk_preamble(const WalkArgs& a, long s, double2* xs, const doubl
     return found;
 }
 
+// Certified parallel form of the same search. Each lag's correlation e is
+// computed exactly as the reference (j = 0..L-1 in order, no FMA); its energy
+// is the window sum s_i = sum_{j<L} E[i+j] taken per lag instead of the
+// serial recurrence n_i. The two differ by at most
+//   |n_i - s_i| <= (2L + 2i + 4) u M  (u = 2^-53, M >= every partial value
+// the recurrence passes through: max window sum + max sample energy), so a
+// lag whose norm test and ratio test both clear their thresholds by more
+// than that bound is decided exactly as the reference decides it. The first
+// lag that is not a certain FAIL is the answer when it is a certain PASS;
+// otherwise (margins ~1e-13, practically never) the exact serial search runs.
+__device__ int walk_preamble(const WalkArgs& a, long s, double2* xs, const double2* c, double* E, double* normv,
+                             int* best, int* unsure, double* mred, int t)
+{
+    constexpr double U = 0x1.0p-53;
+    const int L = a.L, C = a.cycles;
+    if (a.exact_only) return walk_preamble_exact(a, s, xs, c, E, normv, best, t);
+    double emax = 0.0;
+    for (int i = t; i < C + L; i += WALK_THREADS) {
+        const double2 v = stream_sample(a, s + i);
+        xs[i] = v;
+        const double e2 = add_rn(mul_rn(v.x, v.x), mul_rn(v.y, v.y));
+        E[i] = e2;
+        emax = fmax(emax, e2);
+    }
+    if (t == 0) {
+        *best = INT_MAX;
+        *unsure = INT_MAX;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) emax = fmax(emax, __shfl_xor(emax, o));
+    if ((t & 63) == 0) mred[WALK_THREADS / 64 + (t >> 6)] = emax;
+    double M = 0.0;  // max window sum over every lag so far
+    int found = INT_MAX;
+    for (int base = 0; base < C; base += 2 * WALK_THREADS) {
+        __syncthreads();  // xs/E visible (first batch); best/unsure reset
+        // two lags per thread, interleaved (two independent accumulation chains)
+        const int i0 = base + t, i1 = base + WALK_THREADS + t;
+        const bool v0 = i0 < C, v1 = i1 < C;
+        const int j0 = v0 ? i0 : 0, j1 = v1 ? i1 : 0;
+        double2 e0 = make_double2(0.0, 0.0), e1 = make_double2(0.0, 0.0);
+        double s0 = 0.0, s1 = 0.0;
+        for (int j = 0; j < L; ++j) {
+            const double2 cj = c[j];
+            e0 = cadd_rn(e0, cmul_exact(xs[j0 + j], cj));
+            e1 = cadd_rn(e1, cmul_exact(xs[j1 + j], cj));
+            s0 = add_rn(s0, E[j0 + j]);
+            s1 = add_rn(s1, E[j1 + j]);
+        }
+        // M over every lag so far (block max; the bound needs it for all i' <= i)
+        double mloc = fmax(v0 ? s0 : 0.0, v1 ? s1 : 0.0);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mloc = fmax(mloc, __shfl_xor(mloc, o));
+        if ((t & 63) == 0) mred[t >> 6] = mloc;
+        __syncthreads();
+        double mb = mred[0], eb = mred[WALK_THREADS / 64];
+        for (int w = 1; w < WALK_THREADS / 64; ++w) {
+            mb = fmax(mb, mred[w]);
+            eb = fmax(eb, mred[WALK_THREADS / 64 + w]);
+        }
+        M = fmax(M, mb);
+        const double Mall = M + eb;  // bounds every partial value of the recurrence
+        auto decide = [&](int i, double2 e, double sn) {
+            // 0 = certain FAIL, 1 = certain PASS, 2 = uncertain
+            const double B = (2.0 * L + 2.0 * i + 8.0) * U * (Mall + sn) * 1.25;
+            if (sn + B <= 1.0) return 0;           // n_i <= 1 for sure
+            const bool norm_ok = sn - B > 1.0;     // n_i > 1 for sure
+            const double r = hypot(e.x, e.y) / sqrt(sn);
+            const double d = (sn - B > 0.0 ? B / (sn - B) : 1.0) * 0.5 + 16.0 * U;
+            if (r * (1.0 + d) <= a.pr_level) return 0;
+            if (norm_ok && r * (1.0 - d) > a.pr_level) return 1;
+            return 2;
+        };
+        if (v0) {
+            const int d0 = decide(i0, e0, s0);
+            if (d0) atomicMin(best, i0);
+            if (d0 == 2) atomicMin(unsure, i0);
+        }
+        if (v1) {
+            const int d1 = decide(i1, e1, s1);
+            if (d1) atomicMin(best, i1);
+            if (d1 == 2) atomicMin(unsure, i1);
+        }
+        __syncthreads();
+        found = *best;
+        const int un = *unsure;
+        if (found != INT_MAX) {  // uniform
+            __syncthreads();     // every thread has read best/unsure
+            if (un == found) return walk_preamble_exact(a, s, xs, c, E, normv, best, t);
+            return found;
+        }
+    }
+    __syncthreads();
+    return found;
+}
+
 }  // namespace
 
 template <int LOGT>
@@ -917,16 +1013,21 @@ __global__ void __launch_bounds__(WALK_THREADS) stream_walk_kernel(WalkArgs a)
     constexpr int N = 1 << LOGT, T = N / 8, G = WALK_THREADS / T;
     static_assert(T <= WALK_THREADS, "T2sin_size <= 2048");
     constexpr int NW = T >= 64 ? T / 64 : 1;  // waves per transform
+    // LDS: the T2 transforms and the preamble search run one after the other,
+    // so their buffers alias (walk_lds_big): 4 walkers fit a CU
     extern __shared__ double2 smem[];
     double2* lds_tw = smem;
-    double2* fftb = lds_tw + TwLds<LOGT>::SIZE;         // G * N
-    double2* red = fftb + G * N;                        // G * NW (tot, sine)
+    double2* red = lds_tw + TwLds<LOGT>::SIZE;          // G * NW (tot, sine)
     double2* ctap = red + G * NW;                       // L template taps
-    double2* xs = ctap + a.L;                           // cycles + L samples
-    double* E = reinterpret_cast<double*>(xs + a.cycles + a.L);  // cycles + L energies
-    double* normv = E + a.cycles + a.L;                 // cycles running energies
-    int* best = reinterpret_cast<int*>(normv + a.cycles);
+    double* mred = reinterpret_cast<double*>(ctap + a.L);  // 2 * WALK_THREADS/64 maxima
+    int* best = reinterpret_cast<int*>(mred + 2 * (WALK_THREADS / 64));
     int* bestg = best + 1;
+    int* unsure = best + 2;
+    double2* big = reinterpret_cast<double2*>(best + 4);
+    double2* fftb = big;                                // G * N (T2 transforms)
+    double2* xs = big;                                  // cycles + L samples (preamble search)
+    double* E = reinterpret_cast<double*>(xs + a.cycles + a.L);  // cycles + L energies
+    double* normv = E + a.cycles + a.L;                 // cycles running energies (exact fallback)
 
     const int t = threadIdx.x, g = t / T, tt = t - g * T;
     const int c = a.chunk_ids ? a.chunk_ids[blockIdx.x] : (int)blockIdx.x;
@@ -1002,7 +1103,7 @@ __global__ void __launch_bounds__(WALK_THREADS) stream_walk_kernel(WalkArgs a)
             }
         }
         if (stop) break;
-        const int lag = walk_preamble(a, hit, xs, ctap, E, normv, best, t);
+        const int lag = walk_preamble(a, hit, xs, ctap, E, normv, best, unsure, mred, t);
         const long pb = (lag == INT_MAX ? -10 : hit + lag) + 1;  // rx.cpp:160
         if (pb < -2) {                                            // rx.cpp:162-168
             pos = hit + a.msg;
@@ -1033,8 +1134,10 @@ template <int LOGT>
 static hipError_t walk_launch_n(const WalkArgs& a, long nblocks, hipStream_t st)
 {
     constexpr int N = 1 << LOGT, T = N / 8, G = WALK_THREADS / T, NW = T >= 64 ? T / 64 : 1;
-    const size_t shm = sizeof(double2) * (TwLds<LOGT>::SIZE + (size_t)G * N + G * NW + a.L + a.cycles + a.L) +
-                       sizeof(double) * (2 * (size_t)a.cycles + a.L) + 16;
+    const size_t search = sizeof(double2) * ((size_t)a.cycles + a.L) + sizeof(double) * (2 * (size_t)a.cycles + a.L);
+    const size_t big = std::max(sizeof(double2) * (size_t)G * N, search);
+    const size_t shm = sizeof(double2) * (TwLds<LOGT>::SIZE + G * NW + a.L) + sizeof(double) * 2 * (WALK_THREADS / 64) +
+                       16 + big;
     if (shm > 160 * 1024) return hipErrorInvalidValue;
     static bool attr = false;
     if (!attr) {

@@ -91,6 +91,7 @@ struct WalkArgs {
     long* rec;                  // [chunk][max_rec] preamble starts found
     int* nrec;                  // [chunk] frames found (> max_rec: overflow)
     long* exit_pos;             // [chunk] walk state at exit; -1: stream exhausted
+    int exact_only;             // 1: always the serial-recurrence preamble search (test hook, OFDM_WALK_EXACT=1)
 };
 
 struct GatherArgs {

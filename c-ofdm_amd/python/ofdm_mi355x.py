@@ -14,7 +14,8 @@ import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
-LIB_PATH = os.path.join(PKG, "lib", "libofdm_mi355x.so")
+# OFDM_MI355X_LIB: an alternative build of the same library (kernel A/B experiments)
+LIB_PATH = os.environ.get("OFDM_MI355X_LIB") or os.path.join(PKG, "lib", "libofdm_mi355x.so")
 HEADER = os.path.join(os.path.dirname(PKG), "include", "ofdm_mi355x.h")
 
 PARAM_FIELDS = [

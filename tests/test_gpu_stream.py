@@ -98,6 +98,18 @@ def test_stream_config4_matches_sequential_walk(chunk):
     assert len(want) >= 20  # the grid-relative T2 search misses some frames, as the reference does
 
 
+def test_stream_walk_certified_search_equals_serial_recurrence(monkeypatch):
+    # the walker's parallel preamble search (window sums + error bound) against
+    # the reference's serial running-energy recurrence, forced by the test hook
+    x, data = impaired_stream(D, 40, seed=4)
+    fast = run_stream(D, x, chunk=9000)
+    monkeypatch.setenv("OFDM_WALK_EXACT", "1")
+    exact = run_stream(D, x, chunk=9000)
+    assert fast[0] == exact[0]
+    for a, b in zip(fast[1:], exact[1:]):
+        assert np.array_equal(a, b)
+
+
 def test_stream_config_b_and_payload_roundtrip():
     x, data = impaired_stream(B, 12, seed=9, snr_db=30.0, cfo_max=0.001)
     nf, pbs, out, cons, cfo = got = run_stream(B, x, chunk=30000)
