@@ -125,6 +125,9 @@ struct ofdm_ctx {
     double2* d_header = nullptr;   // T2 + preamble
     double2* d_preamble = nullptr; // ofdm_preamble (preamble_len)
     double2* d_templ = nullptr;    // pr_sin_len
+    double2* d_tspec = nullptr;    // WALK_FFT_M template spectrum (stream walker FFT search)
+    double2* d_twm = nullptr;      // WALK_FFT_M twiddles
+    double tspec_max = 0.0;
     double2* d_modpre = nullptr;   // D*npr
     double* d_t2mask = nullptr;    // t2 size
     double2* d_t2tw = nullptr;     // t2-size twiddles (T2 detector)
@@ -287,7 +290,8 @@ int ofdm_destroy(ofdm_ctx* c)
     (void)hipSetDevice(c->device);
     void* ptrs[] = {c->d_tw, c->d_data_bin, c->d_data_slot, c->d_pilot_bin, c->d_bin_map, c->d_rx_pack,
                     c->d_pilot_swz, c->d_tx_code, c->d_const,
-                    c->d_const_bpsk, c->d_header, c->d_preamble, c->d_templ, c->d_modpre, c->d_t2mask,
+                    c->d_const_bpsk, c->d_header, c->d_preamble, c->d_templ, c->d_tspec, c->d_twm, c->d_modpre,
+                    c->d_t2mask,
                     c->d_t2tw, c->d_first, c->d_scratch, c->d_cfo_scratch};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
@@ -509,8 +513,30 @@ int ofdm_create(const ofdm_params* params, int device, ofdm_ctx** out)
             hdr[c->t2 + i] = pre[i];
         }
         for (size_t i = 0; i < tpl.size(); ++i) tpl[i] = make_double2(c->templ[i].real(), c->templ[i].imag());
+        // stream walker FFT search (ofdm_sync.hip walk_preamble_fft): template
+        // spectrum tspec_k = sum_j c_j e^{+2 pi i k j / M}, long double
+        const long cyc = 2 * params->t2sin_size + params->pr_sin_len;
+        std::vector<double2> tsp, twm;
+        if (cyc + params->pr_sin_len <= ofdm::WALK_FFT_M) {
+            const int M = ofdm::WALK_FFT_M;
+            tsp.resize(M);
+            for (int k = 0; k < M; ++k) {
+                long double re = 0, im = 0;
+                for (size_t j = 0; j < c->templ.size(); ++j) {
+                    const long double a = 2.0L * 3.14159265358979323846264338327950288L * (long double)((k * (long)j) % M) / M;
+                    const long double cr = c->templ[j].real(), ci = c->templ[j].imag();
+                    const long double co = cosl(a), si = sinl(a);
+                    re += cr * co - ci * si;
+                    im += cr * si + ci * co;
+                }
+                tsp[k] = make_double2((double)re, (double)im);
+                c->tspec_max = std::max(c->tspec_max, std::hypot(tsp[k].x, tsp[k].y));
+            }
+            twm = twiddles(M);
+        }
         for (size_t i = 0; i < mp.size(); ++i) mp[i] = make_double2(c->mod_preamble[i].real(), c->mod_preamble[i].imag());
-        if ((rc = upload(&c->d_header, hdr)) || (rc = upload(&c->d_preamble, pre)) || (rc = upload(&c->d_templ, tpl)) ||
+        if ((!tsp.empty() && ((rc = upload(&c->d_tspec, tsp)) || (rc = upload(&c->d_twm, twm)))) ||
+            (rc = upload(&c->d_header, hdr)) || (rc = upload(&c->d_preamble, pre)) || (rc = upload(&c->d_templ, tpl)) ||
             (rc = upload(&c->d_modpre, mp)) || (rc = upload(&c->d_t2mask, c->t2_mask))) {
             ofdm_destroy(c);
             return rc;
@@ -1116,6 +1142,9 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
         const char* ex = getenv("OFDM_WALK_EXACT");  // test hook: certified fast search off
         w.exact_only = ex && ex[0] == '1';
     }
+    w.tw_m = c->d_twm;
+    w.tspec = c->d_tspec;  // nullptr: direct certified search
+    w.tspec_max = c->tspec_max;
     w.iq = reinterpret_cast<const double2*>(iq);
     w.iq16 = reinterpret_cast<const short2*>(iq16);
     w.n = nn;

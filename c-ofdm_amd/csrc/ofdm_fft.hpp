@@ -343,6 +343,37 @@ __device__ __forceinline__ void fft_block(double2 (&v)[8], int t, const double2*
     lds_barrier();
 }
 
+// ---------------------------------------------------------------- partial workgroup
+// fft_block run by the first N/8 threads of a larger workgroup: `active` is
+// wave-uniform (N/8 a multiple of 64); every thread takes the barriers.
+template <int LOGN, int PASS, int SIGN>
+__device__ __forceinline__ void fft_tail_active(double2 (&v)[8], int t, const double2* __restrict__ lds_tw,
+                                                double2* __restrict__ lds, bool active)
+{
+    using S = FftShape<LOGN>;
+    constexpr int NPASS = S::NPASS8 + (S::REM ? 1 : 0);
+    if constexpr (PASS < NPASS) {
+        constexpr bool is8 = PASS < S::NPASS8;
+        constexpr int R = is8 ? 8 : (1 << S::REM);
+        constexpr int NS = 1 << (3 * PASS);
+        lds_barrier();
+        if (active) lds_load8<LOGN>(v, t, lds);
+        lds_barrier();
+        if (active) stockham_pass<LOGN, R, NS, SIGN>(v, t, lds_tw, lds);
+        fft_tail_active<LOGN, PASS + 1, SIGN>(v, t, lds_tw, lds, active);
+    }
+}
+
+template <int LOGN, int SIGN>
+__device__ __forceinline__ void fft_block_active(double2 (&v)[8], int t, const double2* __restrict__ lds_tw,
+                                                 double2* __restrict__ lds, bool active)
+{
+    static_assert(LOGN >= 9 && LOGN <= 12, "N/8 must be whole waves");
+    if (active) stockham_pass<LOGN, 8, 1, SIGN>(v, t, lds_tw, lds);
+    fft_tail_active<LOGN, 1, SIGN>(v, t, lds_tw, lds, active);
+    lds_barrier();
+}
+
 // ---------------------------------------------------------------- register output
 // The last Stockham pass (span NS = N/R) writes butterfly b = t + T*u, output
 // r to index b + r*N/R = t + T*(u + r*B): exactly the register v[u + r*B]

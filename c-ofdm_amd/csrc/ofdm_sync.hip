@@ -1005,10 +1005,124 @@ __device__ int walk_preamble(const WalkArgs& a, long s, double2* xs, const doubl
     return found;
 }
 
+// FFT form of the certified search (cycles + L <= M = WALK_FFT_M): all lags'
+// correlations at once as e = IFFT(FFT(x) . tspec) / M (linear correlation:
+// no wrap for i + j < cycles + L <= M), energies as prefix sums. The FFT
+// result differs from the reference's in-order sum by at most
+//   |e^ - e| <= 1024 u ||x||_2 max|tspec|   (~10x the FFT-convolution bound,
+// (2 c log2 M + 1) u ||x|| ||tspec||_inf), and a window energy from two prefix
+// sums from the serial recurrence by (2L + 2i + 8) u (M + s_i) + (4R + 64) u P,
+// so a lag clear of both thresholds by those margins is decided as the
+// reference decides it; the first lag that is not a certain FAIL must be a
+// certain PASS, else the exact search runs. Uses 128 threads for the
+// transforms (fft_block_active); buf: M entries, P: cycles + L doubles.
+__device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double* P, const double2* tw_m,
+                                 double* scr, int* best, int* unsure, double2* xs, double* E, double* normv, int t)
+{
+    constexpr double U = 0x1.0p-53;
+    constexpr int LM = WALK_FFT_LOGM, M = WALK_FFT_M, TM = M / 8;
+    const int L = a.L, C = a.cycles, W = C + L;
+    const bool active = t < TM;
+    double2 v[8];
+    double emax = 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int k = t + TM * i;
+        v[i] = make_double2(0.0, 0.0);
+        if (active && k < W) {
+            v[i] = stream_sample(a, s + k);
+            const double e2 = add_rn(mul_rn(v[i].x, v[i].x), mul_rn(v[i].y, v[i].y));
+            P[k] = e2;
+            emax = fmax(emax, e2);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) emax = fmax(emax, __shfl_xor(emax, o));
+    if ((t & 63) == 0) scr[t >> 6] = emax;
+    if (t == 0) {
+        *best = INT_MAX;
+        *unsure = INT_MAX;
+    }
+    fft_block_active<LM, -1>(v, t, tw_m, buf, active);  // X (barriers: P and scr visible)
+
+    // inclusive prefix sums of P: thread t owns R consecutive entries
+    const int R = (W + WALK_THREADS - 1) / WALK_THREADS;
+    double loc = 0.0;
+    for (int r = 0; r < R; ++r) {
+        const int k = t * R + r;
+        if (k < W) loc += P[k];
+    }
+    double inc = loc;  // wave inclusive scan
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double y = __shfl_up(inc, o);
+        if ((t & 63) >= o) inc += y;
+    }
+    if ((t & 63) == 63) scr[8 + (t >> 6)] = inc;
+    // Y = X . tspec, into registers for the inverse transform
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int k = t + TM * i;
+        if (active) v[i] = cmul(buf[lds_swz(k)], a.tspec[k]);
+    }
+    lds_barrier();  // every thread has read X and the wave totals are visible
+    double run = inc - loc;
+    for (int w = 0; w < (t >> 6); ++w) run += scr[8 + w];
+    for (int r = 0; r < R; ++r) {
+        const int k = t * R + r;
+        if (k < W) {
+            run += P[k];
+            P[k] = run;
+        }
+    }
+    fft_block_active<LM, +1>(v, t, tw_m, buf, active);  // M e_i at buf[lds_swz(i)] (barriers: P final)
+
+    double eb = scr[0];
+    for (int w = 1; w < WALK_THREADS / 64; ++w) eb = fmax(eb, scr[w]);
+    const double ptot = P[W - 1];
+    // max window sum over all lags
+    double mloc = 0.0;
+    for (int i = t; i < C; i += WALK_THREADS) mloc = fmax(mloc, P[i + L - 1] - (i ? P[i - 1] : 0.0));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mloc = fmax(mloc, __shfl_xor(mloc, o));
+    if ((t & 63) == 0) scr[12 + (t >> 6)] = mloc;
+    lds_barrier();
+    double mb = scr[12];
+    for (int w = 1; w < WALK_THREADS / 64; ++w) mb = fmax(mb, scr[12 + w]);
+    const double Mall = (mb + eb) * 1.0625;
+    const double scan_err = (4.0 * R + 64.0) * U * ptot;
+    const double ef = 1024.0 * U * sqrt(ptot * 1.0625) * a.tspec_max;
+    constexpr double inv_m = 1.0 / M;
+    for (int i = t; i < C; i += WALK_THREADS) {
+        const double sn = P[i + L - 1] - (i ? P[i - 1] : 0.0);
+        const double2 e = buf[lds_swz(i)];
+        const double B = (2.0 * L + 2.0 * i + 8.0) * U * (Mall + sn) * 1.25 + scan_err;
+        int d;  // 0 = certain FAIL, 1 = certain PASS, 2 = uncertain
+        if (sn + B <= 1.0) {
+            d = 0;  // n_i <= 1 for sure
+        } else {
+            const double ae = hypot(e.x, e.y) * inv_m;
+            const double r_hi = (ae + ef) / sqrt(fmax(sn - B, 0x1.0p-1000)) * (1.0 + 16.0 * U);
+            const double r_lo = (ae - ef) / sqrt(sn + B) * (1.0 - 16.0 * U);
+            if (r_hi <= a.pr_level)
+                d = 0;
+            else
+                d = (sn - B > 1.0 && r_lo > a.pr_level) ? 1 : 2;
+        }
+        if (d) atomicMin(best, i);
+        if (d == 2) atomicMin(unsure, i);
+    }
+    lds_barrier();
+    const int found = *best, un = *unsure;
+    lds_barrier();  // every thread has read best/unsure
+    if (found != INT_MAX && un == found) return walk_preamble_exact(a, s, xs, a.templ, E, normv, best, t);
+    return found;
+}
+
 }  // namespace
 
 template <int LOGT>
-__global__ void __launch_bounds__(WALK_THREADS) stream_walk_kernel(WalkArgs a)
+__global__ void __launch_bounds__(WALK_THREADS, 4) stream_walk_kernel(WalkArgs a)
 {
     constexpr int N = 1 << LOGT, T = N / 8, G = WALK_THREADS / T;
     static_assert(T <= WALK_THREADS, "T2sin_size <= 2048");
@@ -1023,23 +1137,33 @@ __global__ void __launch_bounds__(WALK_THREADS) stream_walk_kernel(WalkArgs a)
     int* best = reinterpret_cast<int*>(mred + 2 * (WALK_THREADS / 64));
     int* bestg = best + 1;
     int* unsure = best + 2;
-    double2* big = reinterpret_cast<double2*>(best + 4);
+    double* scr = reinterpret_cast<double*>(best + 4);  // 16 scan / max scratch
+    double2* tw_m = reinterpret_cast<double2*>(scr + 16);  // TwLds<WALK_FFT_LOGM> (FFT search)
+    double2* big = tw_m + TwLds<WALK_FFT_LOGM>::SIZE;
     double2* fftb = big;                                // G * N (T2 transforms)
     double2* xs = big;                                  // cycles + L samples (preamble search)
     double* E = reinterpret_cast<double*>(xs + a.cycles + a.L);  // cycles + L energies
     double* normv = E + a.cycles + a.L;                 // cycles running energies (exact fallback)
+    double* P = reinterpret_cast<double*>(big + WALK_FFT_M);  // cycles + L prefix energies (FFT search)
 
-    const int t = threadIdx.x, g = t / T, tt = t - g * T;
+    const int t0 = threadIdx.x;
     const int c = a.chunk_ids ? a.chunk_ids[blockIdx.x] : (int)blockIdx.x;
-    load_twiddles<LOGT>(a.t2tw, lds_tw, t, WALK_THREADS);
-    for (int i = t; i < a.L; i += WALK_THREADS) ctap[i] = a.templ[i];
-    if (t == 0) *bestg = INT_MAX;
+    load_twiddles<LOGT>(a.t2tw, lds_tw, t0, WALK_THREADS);
+    if (a.tspec) load_twiddles<WALK_FFT_LOGM>(a.tw_m, tw_m, t0, WALK_THREADS);
+    for (int i = t0; i < a.L; i += WALK_THREADS) ctap[i] = a.templ[i];
+    if (t0 == 0) *bestg = INT_MAX;
     const long core0 = (long)c * a.chunk, end = core0 + a.chunk;
     long pos = a.start_pos ? a.start_pos[blockIdx.x] : (c == 0 ? 0 : (core0 > a.halo ? core0 - a.halo : 0));
     int nrec = 0;
     long exitp = -1;
     __syncthreads();
     for (;;) {
+        // opaque per-step copy of the thread index: the transforms' LDS
+        // addresses are recomputed per step instead of being hoisted out of
+        // the walk loop and held live (register pressure sets the walkers per CU)
+        int t;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(t0));
+        const int g = t / T, tt = t - g * T;
         if (pos >= end) {
             exitp = pos;
             break;
@@ -1103,7 +1227,9 @@ __global__ void __launch_bounds__(WALK_THREADS) stream_walk_kernel(WalkArgs a)
             }
         }
         if (stop) break;
-        const int lag = walk_preamble(a, hit, xs, ctap, E, normv, best, unsure, mred, t);
+        const int lag = (a.tspec && !a.exact_only)
+                            ? walk_preamble_fft(a, hit, big, P, tw_m, scr, best, unsure, xs, E, normv, t)
+                            : walk_preamble(a, hit, xs, ctap, E, normv, best, unsure, mred, t);
         const long pb = (lag == INT_MAX ? -10 : hit + lag) + 1;  // rx.cpp:160
         if (pb < -2) {                                            // rx.cpp:162-168
             pos = hit + a.msg;
@@ -1114,7 +1240,7 @@ __global__ void __launch_bounds__(WALK_THREADS) stream_walk_kernel(WalkArgs a)
         ++nrec;
         pos = pb + a.msg;  // rx.cpp:192
     }
-    if (t == 0) {
+    if (t0 == 0) {
         a.nrec[c] = nrec;
         a.exit_pos[c] = exitp;
     }
@@ -1135,9 +1261,10 @@ static hipError_t walk_launch_n(const WalkArgs& a, long nblocks, hipStream_t st)
 {
     constexpr int N = 1 << LOGT, T = N / 8, G = WALK_THREADS / T, NW = T >= 64 ? T / 64 : 1;
     const size_t search = sizeof(double2) * ((size_t)a.cycles + a.L) + sizeof(double) * (2 * (size_t)a.cycles + a.L);
-    const size_t big = std::max(sizeof(double2) * (size_t)G * N, search);
+    const size_t fsearch = a.tspec ? sizeof(double2) * WALK_FFT_M + sizeof(double) * ((size_t)a.cycles + a.L) : 0;
+    const size_t big = std::max(std::max(sizeof(double2) * (size_t)G * N, search), fsearch);
     const size_t shm = sizeof(double2) * (TwLds<LOGT>::SIZE + G * NW + a.L) + sizeof(double) * 2 * (WALK_THREADS / 64) +
-                       16 + big;
+                       16 + sizeof(double) * 16 + sizeof(double2) * TwLds<WALK_FFT_LOGM>::SIZE + big;
     if (shm > 160 * 1024) return hipErrorInvalidValue;
     static bool attr = false;
     if (!attr) {

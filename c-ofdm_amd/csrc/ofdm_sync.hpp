@@ -92,7 +92,14 @@ struct WalkArgs {
     int* nrec;                  // [chunk] frames found (> max_rec: overflow)
     long* exit_pos;             // [chunk] walk state at exit; -1: stream exhausted
     int exact_only;             // 1: always the serial-recurrence preamble search (test hook, OFDM_WALK_EXACT=1)
+    // FFT correlation for the preamble search (cycles + L <= WALK_FFT_M): the
+    // template's spectrum and the M-point twiddles, or nullptr (direct search)
+    const double2* tw_m;        // WALK_FFT_M forward twiddles
+    const double2* tspec;       // sum_j c_j e^{+2 pi i k j / M}, k < M
+    double tspec_max;           // max_k |tspec_k| (error bound)
 };
+constexpr int WALK_FFT_LOGM = 10;
+constexpr int WALK_FFT_M = 1 << WALK_FFT_LOGM;
 
 struct GatherArgs {
     const double2* iq;
