@@ -1239,7 +1239,8 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     // copy. Needs the register-window rx and a pilot_freq_sinh plan.
     ofdm_ctx::CfoPlan* pl = nullptr;
     const bool fused = c->S <= ofdm::RX_SMAX && c->D <= ofdm::RX_DPT * (c->N / 8) && c->P <= c->N / 8 &&
-                       c->npr + c->S <= 64 && cfo_plan(c, c->npr, &pl) == OFDM_OK;
+                       c->npr == 1 && c->S + 1 <= 64 && c->L % (c->N / 8) == 0 && c->L / (c->N / 8) <= 16 &&
+                       cfo_plan(c, c->npr, &pl) == OFDM_OK;
     if (fused) {
         const size_t per = (size_t)c->D * sizeof(double2) + (size_t)c->S * 4 * sizeof(double) + sizeof(double);
         const size_t bmax = std::max<size_t>(1, ((size_t)256 << 20) / per);

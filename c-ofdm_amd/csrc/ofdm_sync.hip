@@ -650,14 +650,16 @@ __device__ __forceinline__ double2 src_sample(const double2* iq, const short2* i
 template <int LOGN>
 __global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamParamsArgs a)
 {
+    // one preamble symbol (npr == 1) whose form length L is a multiple of T
+    // (host-checked): thread t holds the preamble form samples t + T*r, r < L/T
     using FS = FftShape<LOGN>;
-    constexpr int N = FS::N, T = FS::T;
+    constexpr int N = FS::N, T = FS::T, RMAX = 16;
     extern __shared__ double2 smem[];
     double2* lds_tw = smem;
     double2* fftb = lds_tw + TwLds<LOGN>::SIZE;   // N
-    double2* pil = fftb + N;                       // npr * P
-    double2* dat = pil + a.npr * a.P;              // D/2 raw bins of symbol 0
-    const int ndat = (a.D / 2 + 1) > (a.npr + a.S) * T ? (a.D / 2 + 1) : (a.npr + a.S) * T;
+    double2* pil = fftb + N;                       // P
+    double2* dat = pil + a.P;                      // D/2 raw bins of the preamble
+    const int ndat = (a.D / 2 + 1) > (1 + a.S) * T ? (a.D / 2 + 1) : (1 + a.S) * T;
     double* ph = reinterpret_cast<double*>(dat + ndat);
     double2* red = reinterpret_cast<double2*>(ph + a.D / 2 + 2);  // 32 entries
     double* phi = reinterpret_cast<double*>(red + 32);            // Q symbol phases
@@ -667,18 +669,29 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamPa
     const long f = blockIdx.x;
     const long x0 = a.starts[f];
     const double cfo = a.cfo[f];
-    const int L = N + a.cp, half = a.D / 2, Q = a.npr + a.S;
-    const long pre = (long)L * a.npr;
+    const int L = N + a.cp, half = a.D / 2, Q = 1 + a.S, LT = L / T, CT = a.cp / T;
+
+    // the preamble form into registers, then the message symbols' CP pairs
+    double2 z[RMAX];
+#pragma unroll
+    for (int r = 0; r < RMAX; ++r)
+        z[r] = r < LT ? src_sample(a.iq, a.iq16, x0 + t + (long)T * r) : make_double2(0.0, 0.0);
     load_twiddles<LOGN>(a.tab.tw, lds_tw, t, T);
 
-    // cp_freq_sinh phases of all Q symbols: per-thread partial sums of every
-    // symbol first (no barrier between symbols, so the loads of several
-    // symbols are in flight together), then one reduction per symbol
+    // cp_freq_sinh phases: per-thread partial sums of every symbol, then one
+    // reduction per symbol (no barrier between symbols: their loads overlap)
     double2* part = dat;  // Q*T partials (dat is filled only later)
     double rs, rc;
     sincospi(-2.0 * cfo * (double)N, &rs, &rc);
-#pragma unroll 3
-    for (int q = 0; q < Q; ++q) {
+    {
+        double2 acc = make_double2(0.0, 0.0);  // preamble: CP sample j = t + T*r, r < cp/T, pairs with r + N/T
+#pragma unroll
+        for (int r = 0; r < RMAX; ++r)
+            if (r < CT && r + N / T < RMAX) acc = cadd(acc, cconj_mul(z[r], z[r + N / T]));
+        part[t] = acc;
+    }
+#pragma unroll 2
+    for (int q = 1; q < Q; ++q) {
         double2 acc = make_double2(0.0, 0.0);
 #pragma unroll 2
         for (int j = t; j < a.cp; j += T) {
@@ -702,21 +715,23 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamPa
             acc += phi[q];
         }
     }
-    __syncthreads();
-    // phase of form sample i = q*L + j before pr_phase_sinh
-    auto theta = [&](int q, int j) {
-        return -2.0 * M_PI * cfo * (double)((long)q * L + j) - (psi[q] * L + phi[q] * j) / N;
-    };
-    // pr_phase_sinh over the whole preamble form
+    // freq_shift + cp_freq_sinh on the preamble: theta(j) = slope * j (psi_0 = 0),
+    // applied as e^{i slope t} * (e^{i slope T})^r
+    const double slope0 = -2.0 * M_PI * cfo - phi[0] / N;
     {
+        double sn, cs, ws, wc;
+        sincos(slope0 * (double)t, &sn, &cs);
+        sincos(slope0 * (double)T, &ws, &wc);
+        double2 c = make_double2(cs, sn);
+        const double2 w = make_double2(wc, ws);
         double2 acc = make_double2(0.0, 0.0);
-#pragma unroll 4
-        for (long i = t; i < pre; i += T) {
-            const int q = (int)(i / L), j = (int)(i - (long)q * L);
-            double sn, cs;
-            sincos(theta(q, j), &sn, &cs);
-            const double2 z = cmul_exact(src_sample(a.iq, a.iq16, x0 + i), make_double2(cs, sn));
-            acc = cadd(acc, cconj_mul(a.pre[i], z));
+#pragma unroll
+        for (int r = 0; r < RMAX; ++r) {
+            if (r < LT) {
+                z[r] = cmul_exact(z[r], c);
+                acc = cadd(acc, cconj_mul(a.pre[t + T * r], z[r]));  // pr_phase_sinh sum
+                c = cmul(c, w);
+            }
         }
         acc = block_sum2<T>(acc, red);
         if (t == 0) phpr = atan2(acc.y, acc.x);
@@ -724,27 +739,30 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamPa
     }
     const double phr = phpr;
 
-    // chan_char_lq: FFT_FORM::read of the corrected preamble symbols
-    for (int s = 0; s < a.npr; ++s) {
+    // chan_char_lq: FFT_FORM::read of the corrected preamble symbol
+    {
+        double sn, cs;
+        sincos(-phr, &sn, &cs);
+        const double2 rot = make_double2(cs, sn);
+        // body sample cp + t + T*i is register CT + i: regrouped through LDS
+        // (CT is a runtime count; a register select chain would cost more)
+#pragma unroll
+        for (int r = 0; r < RMAX; ++r)
+            if (r >= CT && r < LT) fftb[(r - CT) * T + t] = z[r];
+        lds_barrier();
         double2 v[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int j = a.cp + t + T * i;
-            double sn, cs;
-            sincos(theta(s, j) - phr, &sn, &cs);
-            v[i] = cmul_exact(src_sample(a.iq, a.iq16, x0 + (long)s * L + j), make_double2(cs, sn));
-        }
-        __syncthreads();  // fftb free (previous symbol's reads done)
+        for (int i = 0; i < 8; ++i) v[i] = cmul_exact(fftb[t + T * i], rot);
+        lds_barrier();
         fft_block<LOGN, -1>(v, t, lds_tw, fftb);
-        for (int j = t; j < a.P; j += T) pil[s * a.P + j] = fftb[lds_swz(a.tab.pilot_bin[j])];
-        if (s == 0)
-            for (int i = t; i < half; i += T) dat[i] = fftb[lds_swz(a.tab.data_bin[i])];
+        for (int j = t; j < a.P; j += T) pil[j] = fftb[lds_swz(a.tab.pilot_bin[j])];
+        for (int i = t; i < half; i += T) dat[i] = fftb[lds_swz(a.tab.data_bin[i])];
     }
     __syncthreads();
     double acc = 0.0;
-    for (int i = t; i < a.npr * a.P; i += T) acc += hypot(pil[i].x, pil[i].y);
+    for (int i = t; i < a.P; i += T) acc += hypot(pil[i].x, pil[i].y);
     acc = block_sum2<T>(make_double2(acc, 0.0), red).x;
-    const double phys = acc / ((double)(a.P * a.npr) * a.pilot_ampl);
+    const double phys = acc / ((double)a.P * a.pilot_ampl);
     for (int i = t; i < half; i += T) {
         const int j = a.tab.data_slot[i];
         const double2 p0 = make_double2(pil[j].x / phys, pil[j].y / phys);
@@ -787,8 +805,8 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamPa
     }
     // message symbols: theta(m) = A_s + B_s m over the CP-stripped body
     for (int s = t; s < a.S; s += T) {
-        const int q = a.npr + s;
-        const double A = theta(q, a.cp) - phr;
+        const int q = 1 + s;
+        const double A = -2.0 * M_PI * cfo * (double)((long)q * L + a.cp) - (psi[q] * L + phi[q] * a.cp) / N - phr;
         const double B = -2.0 * M_PI * cfo - phi[q] / N;
         double sn, cs;
         sincos(B * T, &sn, &cs);
@@ -804,8 +822,8 @@ template <int LOGN>
 static hipError_t params_launch_n(const StreamParamsArgs& a, hipStream_t st)
 {
     using FS = FftShape<LOGN>;
-    const size_t ndat = std::max<size_t>(a.D / 2 + 1, (size_t)(a.npr + a.S) * FS::T);  // bins, or CP partials
-    const size_t shm = sizeof(double2) * (TwLds<LOGN>::SIZE + FS::N + (size_t)a.npr * a.P + ndat) +
+    const size_t ndat = std::max<size_t>(a.D / 2 + 1, (size_t)(1 + a.S) * FS::T);  // bins, or CP partials
+    const size_t shm = sizeof(double2) * (TwLds<LOGN>::SIZE + FS::N + (size_t)a.P + ndat) +
                        sizeof(double) * (a.D / 2 + 2) + sizeof(double2) * 32 + sizeof(double) * 130;
     if (shm > 160 * 1024) return hipErrorInvalidValue;
     static bool attr = false;
@@ -821,7 +839,9 @@ static hipError_t params_launch_n(const StreamParamsArgs& a, hipStream_t st)
 hipError_t launch_stream_params(int logn, const StreamParamsArgs& a, hipStream_t st)
 {
     if (a.nframes <= 0) return hipSuccess;
-    if (a.npr + a.S > 64) return hipErrorInvalidValue;
+    // one preamble symbol, form length a multiple of T (register layout), <= 16 registers
+    const int T = (1 << logn) / 8, L = (1 << logn) + a.cp;
+    if (a.npr != 1 || a.S + 1 > 64 || L % T != 0 || L / T > 16) return hipErrorInvalidValue;
     switch (logn) {
         case 6: return params_launch_n<6>(a, st);
         case 7: return params_launch_n<7>(a, st);
