@@ -351,7 +351,11 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) tx_kernel(TxArgs a)
                 z.x += w.x;
                 z.y += w.y;
             }
+#ifdef OFDM_TX_PLAIN  // timing experiment only
+            out[j] = z;
+#else
             store_nt(out + j, z);
+#endif
         };
         if (cp_reg) {
 #pragma unroll
@@ -413,7 +417,12 @@ struct SymbolRegs<LOGN, false> {
     {
         constexpr int T = (1 << LOGN) / 8;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) r[i] = load_nt(a.iq + off + t + T * i);
+        for (int i = 0; i < 8; ++i)
+#ifdef OFDM_RX_PLAIN  // timing experiment only
+            r[i] = a.iq[off + t + T * i];
+#else
+            r[i] = load_nt(a.iq + off + t + T * i);
+#endif
     }
     __device__ __forceinline__ double2 get(int i) const { return r[i]; }
 };
@@ -470,7 +479,11 @@ __device__ __forceinline__ void dma_symbol(const RxArgs& a, long off, void* stag
                 "s_mov_b32 %0, m0\n\t"
                 "s_mov_b32 m0, %2\n\t"
                 "s_nop 0\n\t"
+#ifdef OFDM_RX_PLAIN
+                "global_load_lds_dwordx4 %1, off\n\t"
+#else
                 "global_load_lds_dwordx4 %1, off nt\n\t"
+#endif
                 "s_mov_b32 m0, %0"
                 : "=&s"(keep)
                 : "v"(g), "s"(lds)
@@ -523,11 +536,16 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
 #pragma unroll
     for (int i = 0; i < RX_DPT; ++i) pk[i] = a.tab.rx_pack[t0 + T * i];
     const int pbin = a.tab.pilot_swz[t0];
-    long f = blockIdx.x;
+    long fl = blockIdx.x;  // frames in processing order (f: the frame itself)
+#ifdef OFDM_RX_REV  // timing experiment only: frames in reverse order
+    auto frame_of = [&](long l) { return a.nframes - 1 - l; };
+#else
+    auto frame_of = [&](long l) { return l; };
+#endif
     SymbolRegs<LOGN, I16> pf;
     // sample offset of frame g's first message body (CP strip, Frame.hpp:278-279)
     auto body0 = [&](long g) { return SYNC ? a.starts[g] + a.start_off : g * a.frame_stride + a.cp; };
-    dma_symbol<LOGN, I16>(a, body0(f), bufB, t0);  // grid <= nframes
+    dma_symbol<LOGN, I16>(a, body0(frame_of(fl)), bufB, t0);  // grid <= nframes
     if constexpr (kTwSplit) tw_store<LOGN>(twp, lds_tw);
     lds_barrier();  // twiddle table visible: fft_pp reads a pass's twiddles before its barrier
 
@@ -538,7 +556,8 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
     // runs, so HBM reads do not stop between frames, and the tables are
     // loaded once per workgroup.
 #pragma unroll 1
-    for (; f < a.nframes; f += fstep) {
+    for (; fl < a.nframes; fl += fstep) {
+        const long f = frame_of(fl);
         // Opaque per-frame copies of the thread index, the carrier tables and
         // the geometry: everything derived from them is recomputed per frame
         // instead of being hoisted out of the frame loop and held live beside
@@ -593,7 +612,14 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
             // beside the register window
             int tl;
             asm volatile("v_mov_b32 %0, %1" : "=v"(tl) : "v"(t));
+#ifdef OFDM_RX_NOFFT  // timing experiment only: the transform replaced by one LDS hand-off
+            double2* res = first;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) first[lds_swz(tl + T * i)] = v[i];
+            lds_barrier();
+#else
             double2* res = fft_pp<LOGN, -1>(v, tl, lds_tw, first, second);
+#endif
             first = res == bufA ? bufB : bufA;
             second = res;
             if (t < P) pil[s * P + t] = res[pbin];
@@ -619,7 +645,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
             }
         }
         lds_barrier();  // pilots of the last symbol visible; every thread is done reading bufB
-        if (f + fstep < a.nframes) dma_symbol<LOGN, I16>(a, body0(f + fstep), bufB, t);
+        if (fl + fstep < a.nframes) dma_symbol<LOGN, I16>(a, body0(frame_of(fl + fstep)), bufB, t);
 
         // phys_pilot_ampl = sum |pilot| / (P*S*pilot_ampl)   (Frame.cpp:76-80)
         double acc = 0.0;

@@ -110,6 +110,15 @@ def test_stream_walk_certified_search_equals_serial_recurrence(monkeypatch):
         assert np.array_equal(a, b)
 
 
+def test_stream_unfused_decode_path():
+    # num_symb = 12 exceeds the rx register window, so the located frames take
+    # the gather + staged sync chain + staged rx path instead of the fused decode
+    cfg = dict(D, num_symb=12)
+    x, data = impaired_stream(cfg, 12, seed=5)
+    want = check_against_oracle(cfg, x, run_stream(cfg, x, chunk=20000))
+    assert len(want) >= 6
+
+
 def test_stream_config_b_and_payload_roundtrip():
     x, data = impaired_stream(B, 12, seed=9, snr_db=30.0, cfo_max=0.001)
     nf, pbs, out, cons, cfo = got = run_stream(B, x, chunk=30000)

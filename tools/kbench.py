@@ -77,6 +77,20 @@ def main():
                 txm, rxm = alt(noise)
                 print(json.dumps({"config": name, "variant": f"alt tx{'+awgn' if noise else ''} -> rx",
                                   "tx_ms": round(txm, 4), "rx_ms": round(rxm, 4)}), flush=True)
+            # rx after a plain 2.7 GB device write (dirty-line write-back cost seen by the next kernel)
+            junk = torch.empty_like(iq)
+            ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.reps)]
+            for e in ev:
+                e[0].record(st)
+                junk.fill_(1.0)
+                e[1].record(st)
+                m.rx(iq, nf, constell_out=cons, bytes_out=out, ref=data, bit_errors=errs)
+                e[2].record(st)
+            torch.cuda.synchronize()
+            print(json.dumps({"config": name, "variant": "alt fill -> rx",
+                              "fill_ms": round(float(np.median([e[0].elapsed_time(e[1]) for e in ev])), 4),
+                              "rx_ms": round(float(np.median([e[1].elapsed_time(e[2]) for e in ev])), 4)}), flush=True)
+            del junk
         for vname, (fn, nbytes) in variants.items():
             for _ in range(3):
                 fn()
