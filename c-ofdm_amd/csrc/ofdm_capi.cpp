@@ -1116,8 +1116,13 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     const long L = c->L, pre = (long)L * c->npr, msg = (long)L * c->S, span = pre + msg;
     const long flen = c->geo.frame_len, nn = (long)n;
     if (nn == 0) return OFDM_OK;
-    // walkers: at most 4096 chunks, each >= 8 frames; halo of 3 frames to meet the true walk
-    if (chunk <= 0) chunk = std::max(8 * flen, (nn + 4095) / 4096);
+    // walkers: one chunk per resident walker slot (a single round: every
+    // chunk re-walks a 3-frame halo to meet the true walk, so fewer, longer
+    // chunks cost less), each >= 8 frames
+    if (chunk <= 0) {
+        const long slots = ofdm::stream_walk_slots();
+        chunk = std::max(8 * flen, (nn + slots - 1) / slots);
+    }
     chunk = std::max(chunk, (long)c->t2);
     const long halo = 3 * flen;
     const long nchunks = (nn + chunk - 1) / chunk;
@@ -1274,7 +1279,8 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
             sa.cfo = cfo;
             sa.pre = c->d_preamble;
             sa.mod_pre = c->d_modpre;
-            sa.chan_out = chan;
+            sa.chan_out = chan;  // internal scratch: reciprocals for rx's multiply
+            sa.chan_recip = true;
             sa.corr_out = corr;
             sa.npr = c->npr;
             sa.S = c->S;
@@ -1294,6 +1300,7 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
             ra.corr = corr;
             ra.chan = chan;
             ra.chan_stride = c->D;
+            ra.chan_recip = true;
             ra.constell = constell_out ? reinterpret_cast<double2*>(constell_out) + f0 * npts : nullptr;
             ra.bytes = bytes_out ? bytes_out + f0 * c->geo.bytes_per_frame : nullptr;
             ra.S = c->S;

@@ -49,6 +49,7 @@ struct RxArgs {
     long frame_stride;
     const double2* chan;        // nullable: D divisors per frame
     long chan_stride;           // complex elements between frames (0 = shared)
+    bool chan_recip;            // chan holds the divisors' reciprocals (multiply instead of divide)
     double2* constell;          // nullable
     uint8_t* bytes;             // nullable
     const uint8_t* ref;         // nullable

@@ -592,7 +592,10 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
 #pragma unroll
                 for (int i = 0; i < 8; ++i) v[i] = pf.get(i);
             }
-            if (s + 1 < S) pf.load(a, x0 + (long)(s + 1) * L, t);
+            // SYNC: the phase ramp is applied before the next symbol's
+            // prefetch is issued, so its sincos temporaries are not live
+            // beside the 8 prefetch registers (which spilled at N = 512)
+            if (!SYNC && s + 1 < S) pf.load(a, x0 + (long)(s + 1) * L, t);
             if constexpr (SYNC) {
                 // sample m = t + T*i of the body: *= e^{i(A + B m)}, by a
                 // running product from e^{i(A + B t)} in steps of e^{i B T}
@@ -606,6 +609,8 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
                     v[i] = cmul(v[i], c);
                     if (i < 7) c = cmul(c, w);
                 }
+                asm volatile("" ::: "memory");  // keep the prefetch below the ramp
+                if (s + 1 < S) pf.load(a, x0 + (long)(s + 1) * L, t);
             }
             // opaque copy of t: the per-pass LDS addresses are recomputed each
             // symbol instead of being hoisted out of the loop and held live
@@ -671,7 +676,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
             int d = t + T * i, gi = s * P + (pk[i] >> 16);
             asm volatile("" : "+v"(d), "+v"(gi));
             double2 o = cmul_exact(yv, gain[gi]);
-            if (chan) o = cdiv_exact(o, chan[d]);
+            if (chan) o = a.chan_recip ? cmul_exact(o, chan[d]) : cdiv_exact(o, chan[d]);
             if (a.constell) store_nt(a.constell + (f * S + s) * D + d, o);
             dec[whole_frame_dec ? s * D + d : d] = (uint8_t)decide(o, a.k, s1, m);
         };

@@ -659,7 +659,8 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamPa
     double2* fftb = lds_tw + TwLds<LOGN>::SIZE;   // N
     double2* pil = fftb + N;                       // P
     double2* dat = pil + a.P;                      // D/2 raw bins of the preamble
-    const int ndat = (a.D / 2 + 1) > (1 + a.S) * T ? (a.D / 2 + 1) : (1 + a.S) * T;
+    constexpr int NWV = T >= 64 ? T / 64 : 1;      // waves
+    const int ndat = (a.D / 2 + 1) > (1 + a.S) * NWV ? (a.D / 2 + 1) : (1 + a.S) * NWV;
     double* ph = reinterpret_cast<double*>(dat + ndat);
     double2* red = reinterpret_cast<double2*>(ph + a.D / 2 + 2);  // 32 entries
     double* phi = reinterpret_cast<double*>(red + 32);            // Q symbol phases
@@ -678,9 +679,20 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamPa
         z[r] = r < LT ? src_sample(a.iq, a.iq16, x0 + t + (long)T * r) : make_double2(0.0, 0.0);
     load_twiddles<LOGN>(a.tab.tw, lds_tw, t, T);
 
-    // cp_freq_sinh phases: per-thread partial sums of every symbol, then one
-    // reduction per symbol (no barrier between symbols: their loads overlap)
-    double2* part = dat;  // Q*T partials (dat is filled only later)
+    // cp_freq_sinh phases: per-thread partial sums of every symbol, reduced
+    // per wave by shuffles, then across waves in LDS (no barrier between
+    // symbols: their loads overlap)
+    double2* part = dat;  // Q*NWV wave partials (dat is filled only later)
+    const int lane = t & 63, wv = t >> 6;
+    auto wave_part = [&](int q, double2 acc) {
+        constexpr int W0 = T >= 64 ? 32 : T / 2;
+#pragma unroll
+        for (int o = W0; o > 0; o >>= 1) {
+            acc.x += __shfl_xor(acc.x, o);
+            acc.y += __shfl_xor(acc.y, o);
+        }
+        if (lane == 0) part[q * NWV + wv] = acc;
+    };
     double rs, rc;
     sincospi(-2.0 * cfo * (double)N, &rs, &rc);
     {
@@ -688,7 +700,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamPa
 #pragma unroll
         for (int r = 0; r < RMAX; ++r)
             if (r < CT && r + N / T < RMAX) acc = cadd(acc, cconj_mul(z[r], z[r + N / T]));
-        part[t] = acc;
+        wave_part(0, acc);
     }
 #pragma unroll 2
     for (int q = 1; q < Q; ++q) {
@@ -698,12 +710,12 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamPa
             const long i0 = x0 + (long)q * L + j;
             acc = cadd(acc, cconj_mul(src_sample(a.iq, a.iq16, i0), src_sample(a.iq, a.iq16, i0 + N)));
         }
-        part[q * T + t] = acc;
+        wave_part(q, acc);
     }
     __syncthreads();
     for (int q = t; q < Q; q += T) {
         double2 acc = make_double2(0.0, 0.0);
-        for (int u = 0; u < T; ++u) acc = cadd(acc, part[q * T + u]);
+        for (int u = 0; u < NWV; ++u) acc = cadd(acc, part[q * NWV + u]);
         const double2 r = cmul_exact(acc, make_double2(rc, rs));
         phi[q] = atan2(r.y, r.x);
     }
@@ -801,7 +813,9 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamPa
             th = add_rn(add_rn(mul_rn(-b, (double)a.D) / 2, mul_rn((double)(i - half), b)), aa);
         double sn, cs;
         sincos(th, &sn, &cs);
-        chan[i] = make_double2(cs, sn);
+        // the reciprocal once per carrier (libgcc division, as the caller's
+        // constell /= chan would round it) instead of a division per point
+        chan[i] = a.chan_recip ? cdiv_exact(make_double2(1.0, 0.0), make_double2(cs, sn)) : make_double2(cs, sn);
     }
     // message symbols: theta(m) = A_s + B_s m over the CP-stripped body
     for (int s = t; s < a.S; s += T) {
@@ -822,7 +836,7 @@ template <int LOGN>
 static hipError_t params_launch_n(const StreamParamsArgs& a, hipStream_t st)
 {
     using FS = FftShape<LOGN>;
-    const size_t ndat = std::max<size_t>(a.D / 2 + 1, (size_t)(1 + a.S) * FS::T);  // bins, or CP partials
+    const size_t ndat = std::max<size_t>(a.D / 2 + 1, (size_t)(1 + a.S) * (FS::T >= 64 ? FS::T / 64 : 1));  // bins, or CP wave partials
     const size_t shm = sizeof(double2) * (TwLds<LOGN>::SIZE + FS::N + (size_t)a.P + ndat) +
                        sizeof(double) * (a.D / 2 + 2) + sizeof(double2) * 32 + sizeof(double) * 130;
     if (shm > 160 * 1024) return hipErrorInvalidValue;
@@ -1294,6 +1308,19 @@ static hipError_t walk_launch_n(const WalkArgs& a, long nblocks, hipStream_t st)
     }
     hipLaunchKernelGGL(stream_walk_kernel<LOGT>, dim3((unsigned)nblocks), dim3(WALK_THREADS), shm, st, a);
     return hipGetLastError();
+}
+
+long stream_walk_slots()
+{
+    static long cache[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    if (!cache[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cache[dev] = 4L * n;  // __launch_bounds__(WALK_THREADS, 4): 4 walkers per CU
+    }
+    return cache[dev];
 }
 
 hipError_t launch_stream_walk(int logt, const WalkArgs& a, long nblocks, hipStream_t st)

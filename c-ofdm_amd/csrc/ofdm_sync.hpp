@@ -126,6 +126,7 @@ struct StreamParamsArgs {
     const double2* pre;         // ofdm_preamble (npr*L samples)
     const double2* mod_pre;     // D*npr BPSK points
     double2* chan_out;          // nframes * D
+    bool chan_recip;            // write 1/chan (for rx's chan_recip mode) instead of chan
     double* corr_out;           // nframes * S * 4: A_s, B_s, cos(B_s*T), sin(B_s*T)
     int npr, S, D, P, cp;
     double pilot_ampl;
@@ -134,6 +135,8 @@ struct StreamParamsArgs {
 hipError_t launch_stream_params(int logn, const StreamParamsArgs& a, hipStream_t st);
 
 hipError_t launch_stream_walk(int logt, const WalkArgs& a, long nblocks, hipStream_t st);
+// stream walkers resident at once on the current device (4 per CU)
+long stream_walk_slots();
 hipError_t launch_gather(const GatherArgs& a, hipStream_t st);
 hipError_t launch_t2_scan(int logn, const T2Args& a, int* first_out, hipStream_t st);
 hipError_t launch_find_preamble(const PreambleArgs& a, hipStream_t st);

@@ -53,6 +53,8 @@ def main():
             "rx(constell+bytes+ber)": (lambda: m.rx(iq, nf, constell_out=cons, bytes_out=out, ref=data,
                                                    bit_errors=errs), rx_b + nf * S * D * k // 8),
             "rx(bytes)": (lambda: m.rx(iq, nf, bytes_out=out), nf * S * (16 * N + D * k // 8)),
+            # achievable-bandwidth reference: a torch device copy of the constellation's size
+            "torch copy (ref)": (lambda: cons.copy_(iq[:cons.numel()]), 2 * 16 * cons.numel()),
             "rx_i16(constell+bytes+ber)": (lambda: m.rx_i16(iq16, nf, constell_out=cons, bytes_out=out, ref=data,
                                                            bit_errors=errs),
                                           nf * S * (4 * N + 16 * D + D * k // 8) + nf * S * D * k // 8),

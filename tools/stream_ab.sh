@@ -1,0 +1,12 @@
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_stream.py tests/test_gpu_sync.py tests/test_dropin_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/stream_tests.log 2>&1 || exit 1
+for r in 1 2; do
+  for v in head new; do
+    if [ $v = head ]; then export OFDM_MI355X_LIB=exp/libofdm_head.so; else unset OFDM_MI355X_LIB; fi
+    timeout -k 10 120 python tools/stream_bench.py 2>/dev/null | sed "s/^/$v /" >> gpurun_out/stream_ab.txt || exit 1
+    timeout -k 10 120 python tools/stream_bench.py --i16 2>/dev/null | sed "s/^/$v /" >> gpurun_out/stream_ab.txt || exit 1
+  done
+done
+unset OFDM_MI355X_LIB
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/sprof2 -o run -- python3 tools/stream_bench.py --reps 3 > gpurun_out/sprof2.log 2>&1
