@@ -123,7 +123,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=10, help="untimed steps (the GPU clocks ramp over the first ~10 launches)")
     ap.add_argument("--frames", type=int, default=8192, help="frames per GPU (8 symbols each); weak scaling")
     ap.add_argument("--total-frames", type=int, default=0,
                     help="strong scaling: shard this many frames over the GPUs (config 5: 30517 = 10 GB)")
