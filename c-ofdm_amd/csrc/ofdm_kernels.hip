@@ -16,6 +16,7 @@
 //   demap/map   : Modulation::demod / ::mod on flat point arrays.
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 
 #include "ofdm_fft.hpp"
 #include "ofdm_internal.hpp"
@@ -840,6 +841,9 @@ __global__ void f64_to_i16_kernel(const double2* __restrict__ in, long n, double
 }
 
 // ------------------------------------------------------------------ launchers
+static int num_cus();
+static long env_wgs_per_cu(const char* name);
+
 template <int LOGN, bool POINTS, bool NOISE, bool I16>
 static hipError_t tx_launch_n(const TxArgs& a, hipStream_t st)
 {
@@ -854,7 +858,9 @@ static hipError_t tx_launch_n(const TxArgs& a, hipStream_t st)
     const long nsym = a.nframes * a.S;
     if (nsym <= 0) return hipSuccess;
     // persistent grid: enough workgroups to fill every CU several times over
-    const long grid = nsym < TX_MAX_GRID ? nsym : TX_MAX_GRID;
+    long grid = nsym < TX_MAX_GRID ? nsym : TX_MAX_GRID;
+    const long ov = env_wgs_per_cu("OFDM_TX_WGS_PER_CU");
+    if (ov > 0 && ov * num_cus() < grid) grid = ov * num_cus();
     hipLaunchKernelGGL((tx_kernel<LOGN, POINTS, NOISE, I16>), dim3((unsigned)grid), dim3(FS::T), shm, st, a);
     return hipGetLastError();
 }
@@ -899,6 +905,15 @@ static int num_cus()
     return cache[dev];
 }
 
+// Timing experiments (tools/overlap_probe.py): cap a persistent grid at this
+// many workgroups per CU, so a tx and an rx launch can share the CUs. Unset
+// or 0: the occupancy limit.
+static long env_wgs_per_cu(const char* name)
+{
+    const char* e = getenv(name);
+    return e ? atol(e) : 0;
+}
+
 template <int LOGN>
 static size_t rx_shm(const RxArgs& a)
 {
@@ -923,7 +938,10 @@ static hipError_t rx_launch_n(const RxArgs& a, hipStream_t st)
     // window's occupancy: 2 per SIMD), as far as LDS allows
     const long per_cu_w = RX_WAVES_PER_CU / (FS::T >= 64 ? FS::T / 64 : 1);
     const long per_cu_l = (long)(160 * 1024) / (long)shm;
-    const long cap = (per_cu_w < per_cu_l ? per_cu_w : per_cu_l) * num_cus();
+    long per_cu = per_cu_w < per_cu_l ? per_cu_w : per_cu_l;
+    const long ov = env_wgs_per_cu("OFDM_RX_WGS_PER_CU");
+    if (ov > 0 && ov < per_cu) per_cu = ov;
+    const long cap = per_cu * num_cus();
     const long grid = a.nframes < cap ? a.nframes : cap;
     hipLaunchKernelGGL((rx_kernel<LOGN, STAGED, I16, SYNC>), dim3((unsigned)grid), dim3(FS::T), shm, st, a);
     return hipGetLastError();

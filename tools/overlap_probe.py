@@ -71,9 +71,19 @@ def main():
         cur.wait_event(e1)
         cur.wait_event(e2)
 
-    print(json.dumps({"tx_half_ms": timeit(lambda: tx_a(cur.cuda_stream)),
-                      "rx_half_ms": timeit(lambda: rx_b(cur.cuda_stream)),
-                      "sequential_ms": timeit(seq), "two_streams_ms": timeit(par)}))
+    res = {"tx_half_ms": timeit(lambda: tx_a(cur.cuda_stream)),
+           "rx_half_ms": timeit(lambda: rx_b(cur.cuda_stream)),
+           "sequential_ms": timeit(seq), "two_streams_ms": timeit(par)}
+    # co-residency: cap the persistent grids (workgroups per CU) so that both
+    # kernels fit the CUs at once (OFDM_RX_WGS_PER_CU / OFDM_TX_WGS_PER_CU)
+    for rxw, txw in ((1, 1), (1, 2), (2, 1)):
+        os.environ["OFDM_RX_WGS_PER_CU"] = str(rxw)
+        os.environ["OFDM_TX_WGS_PER_CU"] = str(txw)
+        res[f"two_streams_rx{rxw}_tx{txw}_ms"] = timeit(par)
+        res[f"sequential_rx{rxw}_tx{txw}_ms"] = timeit(seq)
+    os.environ.pop("OFDM_RX_WGS_PER_CU")
+    os.environ.pop("OFDM_TX_WGS_PER_CU")
+    print(json.dumps({k: round(v, 4) for k, v in res.items()}))
 
 
 if __name__ == "__main__":

@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--snr-db", type=float, default=20.0)
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--i16", action="store_true", help="wire-format complex<int16> stream (x mult)")
+    ap.add_argument("--cpu-seconds", type=float, default=0.0,
+                    help="also time the oracle's walk + decode on a prefix of the stream (~this many s)")
     args = ap.parse_args()
     import torch
     import ofdm_mi355x as M
@@ -83,13 +85,46 @@ def main():
         ref = data.reshape(nf, -1)[where.clamp(0, nf - 1)]
         ok = int((ref == out.reshape(nf, -1)[:k]).all(dim=1).sum().item())
     ms = float(np.median(times)) * 1e3
-    print(json.dumps({"workload": "config4_stream_D_frames_gaps0-4096_cfo0.004_awgn%gdB%s"
-                                  % (args.snr_db, "_int16" if args.i16 else ""),
-                      "stream_samples": n, "frames_sent": nf, "frames_found": found, "frames_error_free": ok,
-                      "ms": round(ms, 3), "G_stream_samples_per_s": round(n / ms / 1e6, 2),
-                      "frames_per_s": round(found / ms * 1e3), "stream_GB": round(n * (4 if args.i16 else 16) / 1e9, 3),
-                      "chunk": args.chunk}), flush=True)
+    # SURVEY §8d config 4 algorithmic bytes: the stream read once, plus each
+    # located frame's constellation and payload bytes written
+    esz = 4 if args.i16 else 16
+    alg = n * esz + found * (16 * g["npts"] + g["bytes_per_frame"])
+    res = {"workload": "config4_stream_D_frames_gaps0-4096_cfo0.004_awgn%gdB%s"
+                       % (args.snr_db, "_int16" if args.i16 else ""),
+           "stream_samples": n, "frames_sent": nf, "frames_found": found, "frames_error_free": ok,
+           "ms": round(ms, 3), "G_stream_samples_per_s": round(n / ms / 1e6, 2),
+           "frames_per_s": round(found / ms * 1e3), "stream_GB": round(n * esz / 1e9, 3),
+           "chunk": args.chunk,
+           "roofline": {"bound": "hbm", "algorithmic_bytes": alg, "achieved": round(alg / ms / 1e6, 1),
+                        "peak": 8000.0, "unit": "GB/s", "frac": round(alg / ms / 1e6 / 8000.0, 4),
+                        "note": "whole stream pipeline (walk + decode + host stitching) against the "
+                                "bytes it must move once"}}
+    if args.cpu_seconds > 0 and not args.i16:
+        res["cpu_baseline"] = cpu_stream_baseline(cfg, x, args.cpu_seconds)
+    print(json.dumps(res), flush=True)
     m.close()
+
+
+def cpu_stream_baseline(cfg, x, budget_s):
+    """The oracle's rx.cpp walk + main.cpp:60-80 decode, single-threaded as the
+    reference runs, over a prefix of the same stream sized to ~budget_s."""
+    g = O.geometry(cfg)
+    span = g["preamble_len"] + g["message_len"]
+    n = 1 << 18
+    while True:
+        h = x[:n].cpu().numpy()
+        t0 = time.perf_counter()
+        pbs = O.stream_walk(cfg, h)
+        for pb in pbs:
+            if pb + span <= len(h):
+                O.decode_frame(cfg, h[pb:pb + span])
+        dt = time.perf_counter() - t0
+        if dt > budget_s / 4 or n >= len(x):
+            break
+        n = min(len(x), n * 2)
+    return {"value": n / dt, "unit": "stream samples/s", "cores": 1, "kind": "port",
+            "sample": f"oracle orc_stream_walk + orc_decode_frame (own FFT; FFTW absent) over the first "
+                      f"{n} samples ({len(pbs)} frames) of the same stream, {dt:.1f} s, 1 thread"}
 
 
 if __name__ == "__main__":
