@@ -73,6 +73,83 @@ __device__ __forceinline__ double2 block_sum2(double2 v, double2* red)
 
 constexpr int SYNC_THREADS = 256;
 
+// ---------------------------------------------------------------- unwrap
+// chan_char_lq's one-pass unwrap (Frame.hpp:407-414: a phase moves by -/+2 pi
+// when it differs from the already-adjusted previous one by more than pi) as
+// a parallel scan. Entry i's rule maps the previous entry's adjustment
+// k in {-1, 0, +1} (state k+1) to its own, so each entry is a map on 3
+// states, 2 bits per state; maps compose associatively. Per state the same
+// FP64 operations as the serial loop run, so the result is bit-identical.
+constexpr unsigned UMAP_ID = 0u | (1u << 2) | (2u << 4);
+
+__device__ __forceinline__ unsigned umap_then(unsigned f, unsigned g)  // f, then g
+{
+    unsigned h = 0;
+#pragma unroll
+    for (int s = 0; s < 3; ++s) h |= ((g >> (2 * ((f >> (2 * s)) & 3))) & 3) << (2 * s);
+    return h;
+}
+
+// ph[0..n) raw phases in LDS (visible to every thread); on return they are
+// unwrapped and visible. All NT threads call it; scr: NT/64 words of LDS.
+// n - 1 <= 4 * NT (chan_char_lq: n = D/2 <= N/2 = 4 * NT).
+template <int NT>
+__device__ void unwrap_scan(double* ph, int n, unsigned* scr)
+{
+    const int t = threadIdx.x, lane = t & 63;
+    const int R = (n - 1 + NT - 1) / NT;  // entries 1..n-1, R consecutive per thread
+    const int i0 = 1 + t * R;
+    unsigned m[4];
+    double raw[4];
+    unsigned loc = UMAP_ID;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = i0 + r;
+        m[r] = UMAP_ID;
+        raw[r] = 0.0;
+        if (r < R && i < n) {
+            const double x = ph[i], prev = ph[i - 1];
+            raw[r] = x;
+            unsigned mr = 0;
+#pragma unroll
+            for (int st = 0; st < 3; ++st) {
+                const double pa = st == 1 ? prev : (st == 0 ? prev - 2 * M_PI : prev + 2 * M_PI);
+                const double d = x - pa;
+                mr |= (d > M_PI ? 0u : (d < -M_PI ? 2u : 1u)) << (2 * st);
+            }
+            m[r] = mr;
+            loc = umap_then(loc, mr);
+        }
+    }
+    // exclusive scan of the per-thread maps (wave shuffles, then wave totals)
+    unsigned inc = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned y = __shfl_up(inc, o);
+        if (lane >= o) inc = umap_then(y, inc);
+    }
+    unsigned ex = __shfl_up(inc, 1);
+    if (lane == 0) ex = UMAP_ID;
+    if constexpr (NT > 64) {
+        if (lane == 63) scr[t >> 6] = inc;
+        __syncthreads();
+        unsigned pre = UMAP_ID;
+        for (int w = 0; w < (t >> 6); ++w) pre = umap_then(pre, scr[w]);
+        ex = umap_then(pre, ex);
+    }
+    __syncthreads();  // every raw phase has been read
+    int st = (ex >> 2) & 3;  // entry 0 is never adjusted (state 1)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = i0 + r;
+        if (r < R && i < n) {
+            st = (m[r] >> (2 * st)) & 3;
+            ph[i] = st == 1 ? raw[r] : (st == 0 ? raw[r] - 2 * M_PI : raw[r] + 2 * M_PI);
+        }
+    }
+    __syncthreads();
+}
+
 }  // namespace
 
 // ========================================================================
@@ -552,16 +629,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) chan_kernel(ChanArgs a)
         ph[i] = atan2(q.y, q.x);
     }
     __syncthreads();
-    if (t == 0) {  // one-pass unwrap against the already-adjusted previous value (Frame.hpp:407-414)
-        for (int i = 1; i < half; ++i) {
-            const double d = ph[i] - ph[i - 1];
-            if (d > M_PI)
-                ph[i] -= 2 * M_PI;
-            else if (d < -M_PI)
-                ph[i] += 2 * M_PI;
-        }
-    }
-    __syncthreads();
+    unwrap_scan<T>(ph, half, reinterpret_cast<unsigned*>(red) + 96);  // one-pass unwrap (Frame.hpp:407-414)
     double sxy = 0.0, sy = 0.0;
     for (int i = t; i < half; i += T) {
         sxy += ph[i] * i;
@@ -702,15 +770,21 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamPa
             if (r < CT && r + N / T < RMAX) acc = cadd(acc, cconj_mul(z[r], z[r + N / T]));
         wave_part(0, acc);
     }
-#pragma unroll 2
-    for (int q = 1; q < Q; ++q) {
-        double2 acc = make_double2(0.0, 0.0);
+    // two symbols per iteration, so both symbols' CP loads are in flight
+    // together (the shuffles in wave_part keep the compiler from unrolling)
+    for (int q = 1; q < Q; q += 2) {
+        const bool two = q + 1 < Q;  // uniform
+        double2 acc0 = make_double2(0.0, 0.0), acc1 = make_double2(0.0, 0.0);
 #pragma unroll 2
         for (int j = t; j < a.cp; j += T) {
-            const long i0 = x0 + (long)q * L + j;
-            acc = cadd(acc, cconj_mul(src_sample(a.iq, a.iq16, i0), src_sample(a.iq, a.iq16, i0 + N)));
+            const long i0 = x0 + (long)q * L + j, i1 = two ? i0 + L : i0;
+            const double2 a0 = src_sample(a.iq, a.iq16, i0), b0 = src_sample(a.iq, a.iq16, i0 + N);
+            const double2 a1 = src_sample(a.iq, a.iq16, i1), b1 = src_sample(a.iq, a.iq16, i1 + N);
+            acc0 = cadd(acc0, cconj_mul(a0, b0));
+            acc1 = cadd(acc1, cconj_mul(a1, b1));
         }
-        wave_part(q, acc);
+        wave_part(q, acc0);
+        if (two) wave_part(q + 1, acc1);
     }
     __syncthreads();
     for (int q = t; q < Q; q += T) {
@@ -784,16 +858,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamPa
         ph[i] = atan2(q.y, q.x);
     }
     __syncthreads();
-    if (t == 0) {  // one-pass unwrap against the already-adjusted previous value (Frame.hpp:407-414)
-        for (int i = 1; i < half; ++i) {
-            const double d = ph[i] - ph[i - 1];
-            if (d > M_PI)
-                ph[i] -= 2 * M_PI;
-            else if (d < -M_PI)
-                ph[i] += 2 * M_PI;
-        }
-    }
-    __syncthreads();
+    unwrap_scan<T>(ph, half, reinterpret_cast<unsigned*>(red + 24));  // one-pass unwrap (Frame.hpp:407-414)
     double sxy = 0.0, sy = 0.0;
     for (int i = t; i < half; i += T) {
         sxy += ph[i] * i;
