@@ -152,6 +152,11 @@ struct ofdm_ctx {
         size_t bytes = 0;
     };
     Grow s_walk, s_batch, s_chan, s_pbs;
+    // pinned host staging for the walk records and the frame list (pageable
+    // copies go through a driver bounce buffer and synchronise twice)
+    Grow h_walk, h_frames;
+    hipStream_t h_frames_stream = nullptr;  // stream of the last copy out of h_frames
+    bool h_frames_used = false;
 
     ofdm::DevTables tables(bool bpsk) const
     {
@@ -297,6 +302,8 @@ int ofdm_destroy(ofdm_ctx* c)
         if (q) (void)hipFree(q);
     for (auto* g : {&c->s_walk, &c->s_batch, &c->s_chan, &c->s_pbs})
         if (g->p) (void)hipFree(g->p);
+    for (auto* g : {&c->h_walk, &c->h_frames})
+        if (g->p) (void)hipHostFree(g->p);
     for (auto& pl : c->cfo_plans) {
         if (pl.tw_sub) (void)hipFree(pl.tw_sub);
         if (pl.tw_full) (void)hipFree(pl.tw_full);
@@ -674,6 +681,19 @@ static int grow(ofdm_ctx* c, ofdm_ctx::Grow& g, size_t need)
     g.p = nullptr;
     g.bytes = 0;
     HIP_TRY(hipMalloc(&g.p, need));
+    g.bytes = need;
+    return OFDM_OK;
+}
+
+// Pinned host staging that only grows (contents not preserved).
+static int grow_host(ofdm_ctx* c, ofdm_ctx::Grow& g, size_t need)
+{
+    if (need <= g.bytes) return OFDM_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    if (g.p) HIP_TRY(hipHostFree(g.p));
+    g.p = nullptr;
+    g.bytes = 0;
+    HIP_TRY(hipHostMalloc(&g.p, need, hipHostMallocDefault));
     g.bytes = need;
     return OFDM_OK;
 }
@@ -1174,11 +1194,13 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     w.exit_pos = d_exit;
     hipError_t e = ofdm::launch_stream_walk(c->t2_logn, w, nchunks, st);
     if (e != hipSuccess) return hip_fail(e, "stream_walk launch");
-    std::vector<long> rec((size_t)nchunks * max_rec), ex(nchunks);
-    std::vector<int> nrec(nchunks);
-    HIP_TRY(hipMemcpyAsync(rec.data(), d_rec, rec_b, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(ex.data(), d_exit, nchunks * sizeof(long), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(nrec.data(), d_nrec, nchunks * sizeof(int), hipMemcpyDeviceToHost, st));
+    // records, exit states and counts in one copy of the walk buffer's layout
+    if ((rc = grow_host(c, c->h_walk, walk_b))) return rc;
+    char* hb = static_cast<char*>(c->h_walk.p);
+    long* rec = reinterpret_cast<long*>(hb);
+    long* ex = reinterpret_cast<long*>(hb + rec_b);
+    int* nrec = reinterpret_cast<int*>(ex + nchunks + 2);
+    HIP_TRY(hipMemcpyAsync(hb, wb, walk_b, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
 
     // Stitch the chunk walks into the one true walk. Chunk 0 starts at the
@@ -1195,7 +1217,7 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
         r.chunk_ids = d_ids;
         hipError_t e2 = ofdm::launch_stream_walk(c->t2_logn, r, 1, st);
         if (e2 != hipSuccess) return hip_fail(e2, "stream_walk re-walk launch");
-        HIP_TRY(hipMemcpyAsync(rec.data() + (size_t)k * max_rec, d_rec + (size_t)k * max_rec, max_rec * sizeof(long),
+        HIP_TRY(hipMemcpyAsync(rec + (size_t)k * max_rec, d_rec + (size_t)k * max_rec, max_rec * sizeof(long),
                                hipMemcpyDeviceToHost, st));
         HIP_TRY(hipMemcpyAsync(&ex[k], d_exit + k, sizeof(long), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipMemcpyAsync(&nrec[k], d_nrec + k, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -1208,7 +1230,7 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     for (long k = 0; k < nchunks; ++k) {
         if (k > 0 && texit < 0) break;  // the true walk ended
         if (nrec[k] > max_rec) return fail(OFDM_ERR_HIP, "stream walk record overflow");
-        std::vector<long> lst(rec.begin() + (size_t)k * max_rec, rec.begin() + (size_t)k * max_rec + nrec[k]);
+        std::vector<long> lst(rec + (size_t)k * max_rec, rec + (size_t)k * max_rec + nrec[k]);
         const long lo = k * chunk, hi = lo + chunk;
         if (k > 0) {
             long first_owned = LONG_MAX;
@@ -1220,7 +1242,7 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
             if (!sync) {
                 if ((rc = rewalk(k, texit))) return rc;
                 if (nrec[k] > max_rec) return fail(OFDM_ERR_HIP, "stream walk record overflow");
-                lst.assign(rec.begin() + (size_t)k * max_rec, rec.begin() + (size_t)k * max_rec + nrec[k]);
+                lst.assign(rec + (size_t)k * max_rec, rec + (size_t)k * max_rec + nrec[k]);
             }
         }
         for (long pb : lst)
@@ -1233,9 +1255,16 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     if (nout == 0) return OFDM_OK;
 
     // located frames -> main.cpp:60-80 chain + demod
-    if ((rc = grow(c, c->s_pbs, nout * sizeof(long)))) return rc;
+    if ((rc = grow(c, c->s_pbs, nout * sizeof(long))) || (rc = grow_host(c, c->h_frames, nout * sizeof(long))))
+        return rc;
     long* d_pbs = static_cast<long*>(c->s_pbs.p);
-    HIP_TRY(hipMemcpyAsync(d_pbs, frames.data(), nout * sizeof(long), hipMemcpyHostToDevice, st));
+    // the previous call's copy out of the pinned stage must have finished: on
+    // the same stream the walk-record sync above saw to it
+    if (c->h_frames_used && c->h_frames_stream != st) HIP_TRY(hipStreamSynchronize(c->h_frames_stream));
+    c->h_frames_stream = st;
+    c->h_frames_used = true;
+    std::memcpy(c->h_frames.p, frames.data(), nout * sizeof(long));
+    HIP_TRY(hipMemcpyAsync(d_pbs, c->h_frames.p, nout * sizeof(long), hipMemcpyHostToDevice, st));
     if (pb_out) HIP_TRY(hipMemcpyAsync(pb_out, d_pbs, nout * sizeof(long), hipMemcpyDeviceToDevice, st));
 
     // Fused path: three kernels read each frame from the stream in place
