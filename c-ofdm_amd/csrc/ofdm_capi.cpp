@@ -157,6 +157,7 @@ struct ofdm_ctx {
     Grow h_walk, h_frames;
     hipStream_t h_frames_stream = nullptr;  // stream of the last copy out of h_frames
     bool h_frames_used = false;
+    hipEvent_t ev_walk = nullptr;  // walk records landed in h_walk
 
     ofdm::DevTables tables(bool bpsk) const
     {
@@ -304,6 +305,7 @@ int ofdm_destroy(ofdm_ctx* c)
         if (g->p) (void)hipFree(g->p);
     for (auto* g : {&c->h_walk, &c->h_frames})
         if (g->p) (void)hipHostFree(g->p);
+    if (c->ev_walk) (void)hipEventDestroy(c->ev_walk);
     for (auto& pl : c->cfo_plans) {
         if (pl.tw_sub) (void)hipFree(pl.tw_sub);
         if (pl.tw_full) (void)hipFree(pl.tw_full);
@@ -1153,7 +1155,8 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     const int max_rec = (int)((chunk + halo + 2048 + 2 * c->p.t2sin_size + c->p.pr_sin_len) / msg + 4);
     int rc;
     const size_t rec_b = (size_t)nchunks * max_rec * sizeof(long);
-    const size_t walk_b = rec_b + (size_t)nchunks * (sizeof(long) + sizeof(int)) + 2 * sizeof(long) + 64;
+    const size_t walk_b0 = rec_b + (size_t)nchunks * (sizeof(long) + sizeof(int)) + 2 * sizeof(long) + 64;
+    const size_t walk_b = walk_b0 + 2 * (size_t)nchunks * sizeof(int);  // + in-core counts and first indices
     if ((rc = grow(c, c->s_walk, walk_b))) return rc;
     char* wb = static_cast<char*>(c->s_walk.p);
     long* d_rec = reinterpret_cast<long*>(wb);
@@ -1161,6 +1164,8 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     long* d_start = d_exit + nchunks;  // one re-walk start
     int* d_nrec = reinterpret_cast<int*>(d_start + 2);
     int* d_ids = d_nrec + nchunks;     // one re-walk chunk id (in the 64 B slack)
+    int* d_ncore = reinterpret_cast<int*>(wb + walk_b0);
+    int* d_first_in = d_ncore + nchunks;
 
     ofdm::WalkArgs w{};
     {
@@ -1192,8 +1197,95 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     w.rec = d_rec;
     w.nrec = d_nrec;
     w.exit_pos = d_exit;
+    w.ncore = d_ncore;
+    w.first_in = d_first_in;
     hipError_t e = ofdm::launch_stream_walk(c->t2_logn, w, nchunks, st);
     if (e != hipSuccess) return hip_fail(e, "stream_walk launch");
+
+    // Fused decode: three kernels read each frame from the stream in place
+    // (pilot_freq_sinh; the other sync stages' parameters + chan_char_lq;
+    // rx with the corrections applied on load), no frame copy, no corrected
+    // copy. Needs the register-window rx and a pilot_freq_sinh plan.
+    ofdm_ctx::CfoPlan* pl = nullptr;
+    const bool fused = c->S <= ofdm::RX_SMAX && c->D <= ofdm::RX_DPT * (c->N / 8) && c->P <= c->N / 8 &&
+                       c->npr == 1 && c->S + 1 <= 64 && c->L % (c->N / 8) == 0 && c->L / (c->N / 8) <= 16 &&
+                       cfo_plan(c, c->npr, &pl) == OFDM_OK;
+    const size_t per = (size_t)c->D * sizeof(double2) + (size_t)c->S * 4 * sizeof(double) + sizeof(double);
+    const long npts = (long)c->D * c->S;
+    // frames [0, nb) of d_list (device count d_cnt, if set, bounds them further)
+    auto decode_fused = [&](const long* d_list, size_t nb_total, const long* d_cnt) -> int {
+        const size_t bmax = std::max<size_t>(1, ((size_t)256 << 20) / per);
+        const size_t nb0 = std::min(nb_total, bmax);
+        int r2;
+        if ((r2 = grow(c, c->s_chan, nb0 * per))) return r2;
+        double2* chan = static_cast<double2*>(c->s_chan.p);
+        double* corr = reinterpret_cast<double*>(chan + nb0 * c->D);
+        double* cfo_tmp = corr + nb0 * c->S * 4;
+        for (size_t f0 = 0; f0 < nb_total; f0 += nb0) {
+            const size_t nb = std::min(nb0, nb_total - f0);
+            double* cfo = cfo_out ? cfo_out + f0 : cfo_tmp;
+            ofdm::CfoArgs ca{};
+            ca.x = reinterpret_cast<const double2*>(iq);
+            ca.x16 = reinterpret_cast<const short2*>(iq16);
+            ca.starts = d_list + f0;
+            ca.nframes = (long)nb;
+            ca.tw_sub = pl->tw_sub;
+            ca.tw_full = pl->tw_full;
+            ca.borders = pl->borders;
+            ca.P = c->P;
+            ca.cfo_out = cfo;
+            ca.count = d_cnt;  // single batch when set (f0 == 0)
+            hipError_t e2 = ofdm::launch_cfo(pl->logm, pl->g, ca, st);
+            if (e2 != hipSuccess) return hip_fail(e2, "stream cfo launch");
+            ofdm::StreamParamsArgs sa{};
+            sa.tab = c->tables(true);
+            sa.iq = reinterpret_cast<const double2*>(iq);
+            sa.iq16 = reinterpret_cast<const short2*>(iq16);
+            sa.starts = d_list + f0;
+            sa.nframes = (long)nb;
+            sa.cfo = cfo;
+            sa.pre = c->d_preamble;
+            sa.mod_pre = c->d_modpre;
+            sa.chan_out = chan;  // internal scratch: reciprocals for rx's multiply
+            sa.chan_recip = true;
+            sa.corr_out = corr;
+            sa.npr = c->npr;
+            sa.S = c->S;
+            sa.D = c->D;
+            sa.P = c->P;
+            sa.cp = c->cp;
+            sa.pilot_ampl = (double)c->p.pilot_ampl / 1000;
+            sa.count = d_cnt;
+            e2 = ofdm::launch_stream_params(c->logn, sa, st);
+            if (e2 != hipSuccess) return hip_fail(e2, "stream params launch");
+            ofdm::RxArgs ra{};
+            ra.tab = c->tables(false);
+            ra.iq = reinterpret_cast<const double2*>(iq);
+            ra.iq16 = reinterpret_cast<const short2*>(iq16);
+            ra.nframes = (long)nb;
+            ra.starts = d_list + f0;
+            ra.start_off = pre + c->cp;
+            ra.count = d_cnt;
+            ra.corr = corr;
+            ra.chan = chan;
+            ra.chan_stride = c->D;
+            ra.chan_recip = true;
+            ra.constell = constell_out ? reinterpret_cast<double2*>(constell_out) + f0 * npts : nullptr;
+            ra.bytes = bytes_out ? bytes_out + f0 * c->geo.bytes_per_frame : nullptr;
+            ra.S = c->S;
+            ra.D = c->D;
+            ra.P = c->P;
+            ra.seg = c->seg;
+            ra.cp = c->cp;
+            ra.k = c->k;
+            ra.bytes_per_frame = c->geo.bytes_per_frame;
+            ra.pilot_ampl = (double)c->p.pilot_ampl / 1000;
+            e2 = ofdm::launch_rx(c->logn, ra, st, nullptr);
+            if (e2 != hipSuccess) return hip_fail(e2, "stream rx launch");
+        }
+        return OFDM_OK;
+    };
+
     // records, exit states and counts in one copy of the walk buffer's layout
     if ((rc = grow_host(c, c->h_walk, walk_b))) return rc;
     char* hb = static_cast<char*>(c->h_walk.p);
@@ -1201,7 +1293,45 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     long* ex = reinterpret_cast<long*>(hb + rec_b);
     int* nrec = reinterpret_cast<int*>(ex + nchunks + 2);
     HIP_TRY(hipMemcpyAsync(hb, wb, walk_b, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    if (!c->ev_walk) HIP_TRY(hipEventCreateWithFlags(&c->ev_walk, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(c->ev_walk, st));
+    // Speculative decode: every chunk's in-core records, compacted on the
+    // device behind the copy of the walk records, are decoded while the host
+    // stitches the walks. That list is the stitched walk unless a chunk needs
+    // a re-walk (or the walk ends early); then the host's list is decoded
+    // again over it.
+    const size_t ub = std::min(max_frames, (size_t)nchunks * max_rec);
+    const bool spec = fused && ub > 0 && ub * per <= ((size_t)256 << 20);
+    long* d_pbs = nullptr;
+    if (spec) {
+        if ((rc = grow(c, c->s_pbs, (ub + 1) * sizeof(long)))) return rc;
+        d_pbs = static_cast<long*>(c->s_pbs.p);
+        ofdm::CompactArgs ka{};
+        ka.rec = d_rec;
+        ka.ncore = d_ncore;
+        ka.first_in = d_first_in;
+        ka.nchunks = nchunks;
+        ka.max_rec = max_rec;
+        ka.cap = (long)ub;
+        ka.list = d_pbs;
+        ka.list2 = pb_out;
+        ka.count = d_pbs + ub;
+        e = ofdm::launch_compact(ka, st);
+        if (e != hipSuccess) return hip_fail(e, "stream compact launch");
+    }
+    if (spec && (rc = decode_fused(d_pbs, ub, d_pbs + ub))) return rc;
+    HIP_TRY(hipEventSynchronize(c->ev_walk));
+
+    // the speculative list, from the walks as they came back
+    std::vector<long> spec_list;
+    if (spec)
+        for (long k = 0; k < nchunks; ++k) {
+            const long lo = k * chunk, hi = lo + chunk;
+            for (int i = 0; i < std::min(nrec[k], max_rec); ++i) {
+                const long pb = rec[(size_t)k * max_rec + i];
+                if (pb >= lo && pb < hi) spec_list.push_back(pb);
+            }
+        }
 
     // Stitch the chunk walks into the one true walk. Chunk 0 starts at the
     // true initial state. Chunk k is accepted when its walk and the accepted
@@ -1252,12 +1382,14 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     }
     *nframes_out = frames.size();
     const size_t nout = std::min(frames.size(), max_frames);
+    if (spec && frames == spec_list) return OFDM_OK;  // the speculative decode was the true one
     if (nout == 0) return OFDM_OK;
 
     // located frames -> main.cpp:60-80 chain + demod
-    if ((rc = grow(c, c->s_pbs, nout * sizeof(long))) || (rc = grow_host(c, c->h_frames, nout * sizeof(long))))
+    if ((rc = grow(c, c->s_pbs, (std::max(nout, ub) + 1) * sizeof(long))) ||
+        (rc = grow_host(c, c->h_frames, nout * sizeof(long))))
         return rc;
-    long* d_pbs = static_cast<long*>(c->s_pbs.p);
+    d_pbs = static_cast<long*>(c->s_pbs.p);
     // the previous call's copy out of the pinned stage must have finished: on
     // the same stream the walk-record sync above saw to it
     if (c->h_frames_used && c->h_frames_stream != st) HIP_TRY(hipStreamSynchronize(c->h_frames_stream));
@@ -1267,84 +1399,7 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     HIP_TRY(hipMemcpyAsync(d_pbs, c->h_frames.p, nout * sizeof(long), hipMemcpyHostToDevice, st));
     if (pb_out) HIP_TRY(hipMemcpyAsync(pb_out, d_pbs, nout * sizeof(long), hipMemcpyDeviceToDevice, st));
 
-    // Fused path: three kernels read each frame from the stream in place
-    // (pilot_freq_sinh; the other sync stages' parameters + chan_char_lq;
-    // rx with the corrections applied on load), no frame copy, no corrected
-    // copy. Needs the register-window rx and a pilot_freq_sinh plan.
-    ofdm_ctx::CfoPlan* pl = nullptr;
-    const bool fused = c->S <= ofdm::RX_SMAX && c->D <= ofdm::RX_DPT * (c->N / 8) && c->P <= c->N / 8 &&
-                       c->npr == 1 && c->S + 1 <= 64 && c->L % (c->N / 8) == 0 && c->L / (c->N / 8) <= 16 &&
-                       cfo_plan(c, c->npr, &pl) == OFDM_OK;
-    if (fused) {
-        const size_t per = (size_t)c->D * sizeof(double2) + (size_t)c->S * 4 * sizeof(double) + sizeof(double);
-        const size_t bmax = std::max<size_t>(1, ((size_t)256 << 20) / per);
-        const size_t nb0 = std::min(nout, bmax);
-        if ((rc = grow(c, c->s_chan, nb0 * per))) return rc;
-        double2* chan = static_cast<double2*>(c->s_chan.p);
-        double* corr = reinterpret_cast<double*>(chan + nb0 * c->D);
-        double* cfo_tmp = corr + nb0 * c->S * 4;
-        const long npts = (long)c->D * c->S;
-        for (size_t f0 = 0; f0 < nout; f0 += nb0) {
-            const size_t nb = std::min(nb0, nout - f0);
-            double* cfo = cfo_out ? cfo_out + f0 : cfo_tmp;
-            ofdm::CfoArgs ca{};
-            ca.x = reinterpret_cast<const double2*>(iq);
-            ca.x16 = reinterpret_cast<const short2*>(iq16);
-            ca.starts = d_pbs + f0;
-            ca.nframes = (long)nb;
-            ca.tw_sub = pl->tw_sub;
-            ca.tw_full = pl->tw_full;
-            ca.borders = pl->borders;
-            ca.P = c->P;
-            ca.cfo_out = cfo;
-            e = ofdm::launch_cfo(pl->logm, pl->g, ca, st);
-            if (e != hipSuccess) return hip_fail(e, "stream cfo launch");
-            ofdm::StreamParamsArgs sa{};
-            sa.tab = c->tables(true);
-            sa.iq = reinterpret_cast<const double2*>(iq);
-            sa.iq16 = reinterpret_cast<const short2*>(iq16);
-            sa.starts = d_pbs + f0;
-            sa.nframes = (long)nb;
-            sa.cfo = cfo;
-            sa.pre = c->d_preamble;
-            sa.mod_pre = c->d_modpre;
-            sa.chan_out = chan;  // internal scratch: reciprocals for rx's multiply
-            sa.chan_recip = true;
-            sa.corr_out = corr;
-            sa.npr = c->npr;
-            sa.S = c->S;
-            sa.D = c->D;
-            sa.P = c->P;
-            sa.cp = c->cp;
-            sa.pilot_ampl = (double)c->p.pilot_ampl / 1000;
-            e = ofdm::launch_stream_params(c->logn, sa, st);
-            if (e != hipSuccess) return hip_fail(e, "stream params launch");
-            ofdm::RxArgs ra{};
-            ra.tab = c->tables(false);
-            ra.iq = reinterpret_cast<const double2*>(iq);
-            ra.iq16 = reinterpret_cast<const short2*>(iq16);
-            ra.nframes = (long)nb;
-            ra.starts = d_pbs + f0;
-            ra.start_off = pre + c->cp;
-            ra.corr = corr;
-            ra.chan = chan;
-            ra.chan_stride = c->D;
-            ra.chan_recip = true;
-            ra.constell = constell_out ? reinterpret_cast<double2*>(constell_out) + f0 * npts : nullptr;
-            ra.bytes = bytes_out ? bytes_out + f0 * c->geo.bytes_per_frame : nullptr;
-            ra.S = c->S;
-            ra.D = c->D;
-            ra.P = c->P;
-            ra.seg = c->seg;
-            ra.cp = c->cp;
-            ra.k = c->k;
-            ra.bytes_per_frame = c->geo.bytes_per_frame;
-            ra.pilot_ampl = (double)c->p.pilot_ampl / 1000;
-            e = ofdm::launch_rx(c->logn, ra, st, nullptr);
-            if (e != hipSuccess) return hip_fail(e, "stream rx launch");
-        }
-        return OFDM_OK;
-    }
+    if (fused) return decode_fused(d_pbs, nout, nullptr);
 
     // Fallback: gather each frame into a batch, then the staged sync chain + demod
     const size_t fb = (size_t)span * sizeof(double2);
@@ -1353,7 +1408,6 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     if ((rc = grow(c, c->s_batch, nb0 * fb)) || (rc = grow(c, c->s_chan, nb0 * c->D * sizeof(double2)))) return rc;
     double* batch = static_cast<double*>(c->s_batch.p);
     double* chan = static_cast<double*>(c->s_chan.p);
-    const long npts = (long)c->D * c->S;
     for (size_t f0 = 0; f0 < nout; f0 += nb0) {
         const size_t nb = std::min(nb0, nout - f0);
         ofdm::GatherArgs ga{reinterpret_cast<const double2*>(iq), reinterpret_cast<const short2*>(iq16), nn,

@@ -61,6 +61,7 @@ struct RxArgs {
     // (freq_shift + cp_freq_sinh + pr_phase_sinh, ofdm_sync.hip stream_params_kernel)
     const long* starts;         // nullable
     long start_off;
+    const long* count;          // nullable: frames beyond min(*count, nframes) are skipped
     const double* corr;
     int S, D, P, seg, cp, k;
     long bytes_per_frame;

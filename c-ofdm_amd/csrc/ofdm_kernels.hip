@@ -522,6 +522,10 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
     const int t0 = threadIdx.x;
     const int L = N + a.cp;
     const long fstep = gridDim.x;
+    // frames to process: a.nframes, or fewer when the count is device-side
+    // (speculative stream decode); uniform early exit before any prefetch
+    const long nfr = a.count ? min(*a.count, a.nframes) : a.nframes;
+    if ((long)blockIdx.x >= nfr) return;
 
     // table loads first, then symbol 0 of the first frame: every prologue wait
     // below is a counted vmcnt that leaves the symbol prefetch in flight
@@ -539,7 +543,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
     const int pbin = a.tab.pilot_swz[t0];
     long fl = blockIdx.x;  // frames in processing order (f: the frame itself)
 #ifdef OFDM_RX_REV  // timing experiment only: frames in reverse order
-    auto frame_of = [&](long l) { return a.nframes - 1 - l; };
+    auto frame_of = [&](long l) { return nfr - 1 - l; };
 #else
     auto frame_of = [&](long l) { return l; };
 #endif
@@ -557,7 +561,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
     // runs, so HBM reads do not stop between frames, and the tables are
     // loaded once per workgroup.
 #pragma unroll 1
-    for (; fl < a.nframes; fl += fstep) {
+    for (; fl < nfr; fl += fstep) {
         const long f = frame_of(fl);
         // Opaque per-frame copies of the thread index, the carrier tables and
         // the geometry: everything derived from them is recomputed per frame
@@ -651,7 +655,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
             }
         }
         lds_barrier();  // pilots of the last symbol visible; every thread is done reading bufB
-        if (fl + fstep < a.nframes) dma_symbol<LOGN, I16>(a, body0(frame_of(fl + fstep)), bufB, t);
+        if (fl + fstep < nfr) dma_symbol<LOGN, I16>(a, body0(frame_of(fl + fstep)), bufB, t);
 
         // phys_pilot_ampl = sum |pilot| / (P*S*pilot_ampl)   (Frame.cpp:76-80)
         double acc = 0.0;

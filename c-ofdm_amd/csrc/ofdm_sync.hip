@@ -370,6 +370,7 @@ __global__ void __launch_bounds__(G * (1 << LOGM) / 8) cfo_kernel(CfoArgs a)
     int* wsum = reinterpret_cast<int*>(amp + S);          // per-window argmax
     const int tid = threadIdx.x, g = tid / T, t = tid - g * T;
     const long f = blockIdx.x;
+    if (a.count && f >= *a.count) return;  // uniform: past the speculative frame count
     const long x0 = a.starts ? a.starts[f] : f * a.frame_stride;
     load_twiddles<LOGM>(a.tw_sub, lds_tw, tid, NT);
     double2 v[8];
@@ -736,6 +737,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamPa
     double& phpr = psi[64];  // (dynamic LDS only: the 160 KiB attribute leaves no room for static)
     const int t = threadIdx.x;
     const long f = blockIdx.x;
+    if (a.count && f >= *a.count) return;  // uniform: past the speculative frame count
     const long x0 = a.starts[f];
     const double cfo = a.cfo[f];
     const int L = N + a.cp, half = a.D / 2, Q = 1 + a.S, LT = L / T, CT = a.cp / T;
@@ -1253,7 +1255,7 @@ __global__ void __launch_bounds__(WALK_THREADS, 4) stream_walk_kernel(WalkArgs a
     if (t0 == 0) *bestg = INT_MAX;
     const long core0 = (long)c * a.chunk, end = core0 + a.chunk;
     long pos = a.start_pos ? a.start_pos[blockIdx.x] : (c == 0 ? 0 : (core0 > a.halo ? core0 - a.halo : 0));
-    int nrec = 0;
+    int nrec = 0, ncore = 0, first_in = 0;
     long exitp = -1;
     __syncthreads();
     for (;;) {
@@ -1336,12 +1338,20 @@ __global__ void __launch_bounds__(WALK_THREADS, 4) stream_walk_kernel(WalkArgs a
         }
         if (pb + a.pre + a.msg > a.n) break;  // frame not in the stream: the walk ends
         if (t == 0 && nrec < a.max_rec) a.rec[(long)c * a.max_rec + nrec] = pb;
+        if (pb >= core0 && pb < end) {  // in this chunk's core: one contiguous run of records
+            if (ncore == 0) first_in = nrec;
+            ++ncore;
+        }
         ++nrec;
         pos = pb + a.msg;  // rx.cpp:192
     }
     if (t0 == 0) {
         a.nrec[c] = nrec;
         a.exit_pos[c] = exitp;
+        if (a.ncore) {
+            a.ncore[c] = ncore;
+            a.first_in[c] = first_in;
+        }
     }
 }
 
@@ -1400,6 +1410,81 @@ hipError_t launch_stream_walk(int logt, const WalkArgs& a, long nblocks, hipStre
         case 11: return walk_launch_n<11>(a, nblocks, st);
         default: return hipErrorInvalidValue;
     }
+}
+
+// One workgroup: blocks of 1024 chunks; an exclusive scan of their in-core
+// record counts, then the block's records are copied in parallel.
+__global__ void __launch_bounds__(1024) compact_kernel(CompactArgs a)
+{
+    constexpr int G = 16;
+    __shared__ long excl[1024];  // exclusive scan of the block's counts
+    __shared__ long srcb[1024];  // rec index of each chunk's first in-core record
+    __shared__ long wsum[16];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const long* __restrict__ rec = a.rec;
+    long base = 0;
+    for (long k0 = 0; k0 < a.nchunks; k0 += 1024) {
+        const long k = k0 + t;
+        // only stored records: an overflowing walk (nrec > max_rec) kept the
+        // first max_rec, the host rejects it, and nothing past them is read
+        long cnt = 0, src = 0;  // src: rec index of the chunk's first in-core record
+        if (k < a.nchunks) {
+            const int fi = a.first_in[k];
+            cnt = max(0, min(a.ncore[k], a.max_rec - fi));
+            src = k * a.max_rec + fi;
+        }
+        long inc = cnt;  // inclusive scan: wave, then wave totals
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const long y = __shfl_up(inc, o);
+            if (lane >= o) inc += y;
+        }
+        if (lane == 63) wsum[w] = inc;
+        __syncthreads();
+        long off = inc - cnt;
+        for (int u = 0; u < w; ++u) off += wsum[u];
+        long tot = 0;
+        for (int u = 0; u < 16; ++u) tot += wsum[u];
+        excl[t] = off;
+        srcb[t] = src;
+        __syncthreads();
+        // output slot -> chunk by binary search over the scan; each thread
+        // gathers G records before storing any, so the loads overlap
+        const int nb = (int)min(1024L, a.nchunks - k0);
+        for (long i0 = 0; i0 < tot; i0 += 1024 * G) {
+            long pbv[G];
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const long idx = i0 + g * 1024 + t;
+                pbv[g] = 0;
+                if (idx < tot) {
+                    int lo = 0, hi = nb;  // last j with excl[j] <= idx
+                    while (hi - lo > 1) {
+                        const int mid = (lo + hi) >> 1;
+                        if (excl[mid] <= idx) lo = mid; else hi = mid;
+                    }
+                    pbv[g] = rec[srcb[lo] + (idx - excl[lo])];
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const long idx = i0 + g * 1024 + t, out = base + idx;
+                if (idx < tot && out < a.cap) {
+                    a.list[out] = pbv[g];
+                    if (a.list2) a.list2[out] = pbv[g];
+                }
+            }
+        }
+        base += tot;
+        __syncthreads();  // excl / srcb / wsum are rewritten by the next block
+    }
+    if (t == 0) *a.count = base;
+}
+
+hipError_t launch_compact(const CompactArgs& a, hipStream_t st)
+{
+    hipLaunchKernelGGL(compact_kernel, dim3(1), dim3(1024), 0, st, a);
+    return hipGetLastError();
 }
 
 hipError_t launch_gather(const GatherArgs& a, hipStream_t st)

@@ -41,6 +41,7 @@ struct CfoArgs {
     const int* borders;      // P + 2 window borders (Frame.hpp:311-321)
     int P;
     double* cfo_out;
+    const long* count;       // nullable: frames beyond min(*count, nframes) are skipped (speculative stream decode)
 };
 
 struct ShiftArgs {
@@ -91,6 +92,8 @@ struct WalkArgs {
     long* rec;                  // [chunk][max_rec] preamble starts found
     int* nrec;                  // [chunk] frames found (> max_rec: overflow)
     long* exit_pos;             // [chunk] walk state at exit; -1: stream exhausted
+    int* ncore;                 // nullable: [chunk] records inside the chunk's own core (a contiguous run:
+    int* first_in;              //   the walk only moves forward) and the index of the first of them
     int exact_only;             // 1: always the serial-recurrence preamble search (test hook, OFDM_WALK_EXACT=1)
     // FFT correlation for the preamble search (cycles + L <= WALK_FFT_M): the
     // template's spectrum and the M-point twiddles, or nullptr (direct search)
@@ -130,7 +133,24 @@ struct StreamParamsArgs {
     double* corr_out;           // nframes * S * 4: A_s, B_s, cos(B_s*T), sin(B_s*T)
     int npr, S, D, P, cp;
     double pilot_ampl;
+    const long* count;          // nullable: frames beyond min(*count, nframes) are skipped
 };
+
+// Speculative frame list of a stream walk: every chunk's records inside its
+// own core [k*chunk, (k+1)*chunk), in chunk order, which is the stitched walk
+// whenever no chunk needed a re-walk (the host checks and redoes otherwise).
+struct CompactArgs {
+    const long* rec;            // [chunk][max_rec]
+    const int* ncore;           // [chunk] in-core records (WalkArgs::ncore)
+    const int* first_in;        // [chunk] index of the first of them
+    long nchunks;
+    int max_rec;
+    long cap;                   // list capacity (max_frames)
+    long* list;                 // cap entries
+    long* list2;                // nullable: a second copy (the caller's pb_out)
+    long* count;                // total located (uncapped)
+};
+hipError_t launch_compact(const CompactArgs& a, hipStream_t st);
 
 hipError_t launch_stream_params(int logn, const StreamParamsArgs& a, hipStream_t st);
 
