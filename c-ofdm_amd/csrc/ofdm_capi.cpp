@@ -1141,23 +1141,31 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     // walkers: one chunk per resident walker slot (a single round: every
     // chunk re-walks a 3-frame halo to meet the true walk, so fewer, longer
     // chunks cost less), each >= 8 frames
-    if (chunk <= 0) {
-        const long slots = ofdm::stream_walk_slots();
-        chunk = std::max(8 * flen, (nn + slots - 1) / slots);
-    }
+    const long slots = ofdm::stream_walk_slots();
+    // Knobs (environment, for experiments and tests): chunks per walker slot,
+    // walk-in halo and walk-on extension in 1/1000 frames. Defaults: one
+    // chunk per slot, 3-frame halo, no extension (tools/walk_q_sweep.sh:
+    // 1.5-frame halos with a 2-frame extension, or 2-3 chunks per slot, gain
+    // nothing measurable on config 4; shorter halos force re-walks).
+    const char* eq = getenv("OFDM_WALK_Q");
+    const char* eh = getenv("OFDM_WALK_HALO");
+    const long qper = eq ? std::max(1L, atol(eq)) : 1;
+    if (chunk <= 0) chunk = std::max(8 * flen, (nn + slots * qper - 1) / (slots * qper));
     chunk = std::max(chunk, (long)c->t2);
-    const long halo = 3 * flen;
+    const long halo = eh ? std::max(0L, atol(eh)) * flen / 1000 : 3 * flen;
+    const char* ee = getenv("OFDM_WALK_EXT");
+    const long ext = ee ? std::max(0L, atol(ee)) * flen / 1000 : 0;
     const long nchunks = (nn + chunk - 1) / chunk;
     if (nchunks > 1 << 20) return fail(OFDM_ERR_INVALID, "chunk too small for this stream");
     // each located frame advances the walk by > message_len, and a walker can
-    // overshoot its core end by one scan step (256 threads x 8 samples) plus
-    // the preamble window: this many records always suffice
-    const int max_rec = (int)((chunk + halo + 2048 + 2 * c->p.t2sin_size + c->p.pr_sin_len) / msg + 4);
+    // walk on past its core end by ext plus one scan step (256 threads x 8
+    // samples) and the preamble window: this many records always suffice
+    const int max_rec = (int)((chunk + halo + ext + 2048 + 2 * c->p.t2sin_size + c->p.pr_sin_len) / msg + 4);
     int rc;
     const size_t rec_b = (size_t)nchunks * max_rec * sizeof(long);
     const size_t walk_b0 = rec_b + (size_t)nchunks * (sizeof(long) + sizeof(int)) + 2 * sizeof(long) + 64;
     const size_t walk_b = walk_b0 + 2 * (size_t)nchunks * sizeof(int);  // + in-core counts and first indices
-    if ((rc = grow(c, c->s_walk, walk_b))) return rc;
+    if ((rc = grow(c, c->s_walk, walk_b + 64))) return rc;  // + the chunk queue counter (not copied out)
     char* wb = static_cast<char*>(c->s_walk.p);
     long* d_rec = reinterpret_cast<long*>(wb);
     long* d_exit = reinterpret_cast<long*>(wb + rec_b);
@@ -1193,13 +1201,19 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     w.msg = msg;
     w.chunk = chunk;
     w.halo = halo;
+    w.ext = ext;
     w.max_rec = max_rec;
     w.rec = d_rec;
     w.nrec = d_nrec;
     w.exit_pos = d_exit;
     w.ncore = d_ncore;
     w.first_in = d_first_in;
-    hipError_t e = ofdm::launch_stream_walk(c->t2_logn, w, nchunks, st);
+    // the walkers take chunks from a queue: one resident round of workgroups
+    // drains it, slower walkers taking fewer chunks
+    w.queue = reinterpret_cast<int*>(wb + walk_b);
+    w.nchunks = nchunks;
+    HIP_TRY(hipMemsetAsync(w.queue, 0, sizeof(int), st));
+    hipError_t e = ofdm::launch_stream_walk(c->t2_logn, w, std::min(nchunks, slots), st);
     if (e != hipSuccess) return hip_fail(e, "stream_walk launch");
 
     // Fused decode: three kernels read each frame from the stream in place
@@ -1338,6 +1352,7 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     // walk before it locate a common frame no later than k's first owned
     // frame (from there on both are the same computation); otherwise it is
     // re-walked from the previous exit state (exact), with one workgroup.
+    long nrewalk = 0;
     auto rewalk = [&](long k, long start) -> int {
         ofdm::WalkArgs r = w;
         const int id = (int)k;
@@ -1345,6 +1360,8 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
         HIP_TRY(hipMemcpyAsync(d_ids, &id, sizeof(int), hipMemcpyHostToDevice, st));
         r.start_pos = d_start;
         r.chunk_ids = d_ids;
+        r.queue = nullptr;
+        ++nrewalk;
         hipError_t e2 = ofdm::launch_stream_walk(c->t2_logn, r, 1, st);
         if (e2 != hipSuccess) return hip_fail(e2, "stream_walk re-walk launch");
         HIP_TRY(hipMemcpyAsync(rec + (size_t)k * max_rec, d_rec + (size_t)k * max_rec, max_rec * sizeof(long),
@@ -1381,6 +1398,9 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
         texit = ex[k];
     }
     *nframes_out = frames.size();
+    if (getenv("OFDM_STREAM_DEBUG"))
+        fprintf(stderr, "ofdm_rx_stream: %ld chunks of %ld samples, halo %ld, %ld re-walks, %zu frames, speculative %s\n",
+                nchunks, chunk, halo, nrewalk, frames.size(), spec ? (frames == spec_list ? "hit" : "miss") : "off");
     const size_t nout = std::min(frames.size(), max_frames);
     if (spec && frames == spec_list) return OFDM_OK;  // the speculative decode was the true one
     if (nout == 0) return OFDM_OK;

@@ -950,6 +950,15 @@ hipError_t launch_stream_params(int logn, const StreamParamsArgs& a, hipStream_t
 // ========================================================================
 namespace {
 
+#ifdef OFDM_WALK_PROF  // timing experiment only: per-walker phase clocks
+__device__ unsigned long long g_walk_prof[8192 * 8];
+__device__ unsigned long long g_walk_fallbacks;
+__device__ unsigned long long g_walk_sub[8192 * 8];  // sub-phase clocks per walker
+#define WPROF(...) __VA_ARGS__
+#else
+#define WPROF(...)
+#endif
+
 constexpr int WALK_THREADS = 256;
 
 // Stream sample j as complex<double> (int16 wire samples convert exactly, as
@@ -1124,6 +1133,7 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
     constexpr int LM = WALK_FFT_LOGM, M = WALK_FFT_M, TM = M / 8;
     const int L = a.L, C = a.cycles, W = C + L;
     const bool active = t < TM;
+    WPROF(const unsigned long long q0 = clock64();)
     double2 v[8];
     double emax = 0.0;
 #pragma unroll
@@ -1145,6 +1155,7 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
         *unsure = INT_MAX;
     }
     fft_block_active<LM, -1>(v, t, tw_m, buf, active);  // X (barriers: P and scr visible)
+    WPROF(const unsigned long long q1 = clock64();)
 
     // inclusive prefix sums of P: thread t owns R consecutive entries
     const int R = (W + WALK_THREADS - 1) / WALK_THREADS;
@@ -1176,7 +1187,9 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
             P[k] = run;
         }
     }
+    WPROF(const unsigned long long q2 = clock64();)
     fft_block_active<LM, +1>(v, t, tw_m, buf, active);  // M e_i at buf[lds_swz(i)] (barriers: P final)
+    WPROF(const unsigned long long q3 = clock64();)
 
     double eb = scr[0];
     for (int w = 1; w < WALK_THREADS / 64; ++w) eb = fmax(eb, scr[w]);
@@ -1216,7 +1229,15 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
     lds_barrier();
     const int found = *best, un = *unsure;
     lds_barrier();  // every thread has read best/unsure
-    if (found != INT_MAX && un == found) return walk_preamble_exact(a, s, xs, a.templ, E, normv, best, t);
+    WPROF(if (t == 0 && blockIdx.x < 8192) {
+        unsigned long long* q = g_walk_sub + 8 * blockIdx.x;
+        const unsigned long long q4 = clock64();
+        q[0] += q1 - q0; q[1] += q2 - q1; q[2] += q3 - q2; q[3] += q4 - q3;
+    })
+    if (found != INT_MAX && un == found) {
+        WPROF(if (t == 0) atomicAdd(&g_walk_fallbacks, 1ULL));
+        return walk_preamble_exact(a, s, xs, a.templ, E, normv, best, t);
+    }
     return found;
 }
 
@@ -1247,16 +1268,33 @@ __global__ void __launch_bounds__(WALK_THREADS, 4) stream_walk_kernel(WalkArgs a
     double* normv = E + a.cycles + a.L;                 // cycles running energies (exact fallback)
     double* P = reinterpret_cast<double*>(big + WALK_FFT_M);  // cycles + L prefix energies (FFT search)
 
+    int* qslot = best + 3;  // the chunk taken from the queue
     const int t0 = threadIdx.x;
-    const int c = a.chunk_ids ? a.chunk_ids[blockIdx.x] : (int)blockIdx.x;
     load_twiddles<LOGT>(a.t2tw, lds_tw, t0, WALK_THREADS);
     if (a.tspec) load_twiddles<WALK_FFT_LOGM>(a.tw_m, tw_m, t0, WALK_THREADS);
     for (int i = t0; i < a.L; i += WALK_THREADS) ctap[i] = a.templ[i];
     if (t0 == 0) *bestg = INT_MAX;
+    WPROF(unsigned long long p_t2 = 0, p_n2 = 0, p_pre = 0, p_np = 0, p_steps = 0;
+          const unsigned long long p_w0 = wall_clock64(); const unsigned long long p_c0 = clock64();)
+    // chunks: from the queue until it is drained (walkers that run slower on
+    // their CU take fewer), or the workgroup's one chunk
+    for (int round = 0;; ++round) {
+    int c;
+    if (a.queue) {
+        if (t0 == 0) *qslot = atomicAdd(a.queue, 1);
+        __syncthreads();
+        c = *qslot;
+        __syncthreads();  // every thread has read the slot
+        if ((long)c >= a.nchunks) break;
+    } else {
+        if (round > 0) break;
+        c = a.chunk_ids ? a.chunk_ids[blockIdx.x] : (int)blockIdx.x;
+    }
     const long core0 = (long)c * a.chunk, end = core0 + a.chunk;
     long pos = a.start_pos ? a.start_pos[blockIdx.x] : (c == 0 ? 0 : (core0 > a.halo ? core0 - a.halo : 0));
     int nrec = 0, ncore = 0, first_in = 0;
     long exitp = -1;
+    bool past = false;  // a frame at or past the core end is located
     __syncthreads();
     for (;;) {
         // opaque per-step copy of the thread index: the transforms' LDS
@@ -1265,29 +1303,42 @@ __global__ void __launch_bounds__(WALK_THREADS, 4) stream_walk_kernel(WalkArgs a
         int t;
         asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(t0));
         const int g = t / T, tt = t - g * T;
+        // The exit state is the first walk state at or past the core end, or
+        // the state whose step located the first frame past it (a re-walk of
+        // the next chunk starts there). The walk goes on until it
+        // has located the first frame at or past the end (within a.ext), so
+        // the next chunk's first frame is in this chunk's records whenever the
+        // two walks agree: a short halo then suffices to meet the true walk.
         if (pos >= end) {
-            exitp = pos;
-            break;
+            if (exitp < 0) exitp = pos;
+            if (past || pos >= end + a.ext) break;
         }
+        const long spos = pos;  // this step's start state
         // find_t2sin(pos): blocks pos + k*N, G per step, first hit wins
         long hit = -1;
         bool stop = false;
+        WPROF(++p_steps; unsigned long long p_a = clock64();)
         for (long base = pos;; base += (long)G * N) {
+            WPROF(++p_n2;)
             if (base + N > a.n) {  // no full block left: the walk has consumed the stream
                 stop = true;
                 break;
             }
-            if (base >= end) {  // scanning past the core: equivalent state, hand over
-                exitp = base;
-                stop = true;
-                break;
+            if (base >= end) {  // scanning past the core: an equivalent state
+                if (exitp < 0) exitp = base;
+                if (base >= end + a.ext) {
+                    stop = true;
+                    break;
+                }
             }
             const long b = base + (long)g * N;
             const bool live = b + N <= a.n;
             double2 v[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) v[i] = live ? stream_sample(a, b + tt + T * i) : make_double2(0.0, 0.0);
+            WPROF(const unsigned long long r0 = clock64();)
             fft_block<LOGT, -1>(v, tt, lds_tw, fftb + g * N);
+            WPROF(const unsigned long long r1 = clock64();)
             double tot = 0.0, sine = 0.0;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
@@ -1322,15 +1373,22 @@ __global__ void __launch_bounds__(WALK_THREADS, 4) stream_walk_kernel(WalkArgs a
             const int bg = *bestg;
             __syncthreads();  // all have read bestg
             if (t == 0) *bestg = INT_MAX;
+            WPROF(if (t == 0 && blockIdx.x < 8192) {
+                unsigned long long* q = g_walk_sub + 8 * blockIdx.x;
+                q[4] += r1 - r0; q[5] += clock64() - r1;
+            })
             if (bg != INT_MAX) {
                 hit = base + (long)bg * N;
                 break;
             }
         }
+        WPROF(unsigned long long p_b = clock64(); p_t2 += p_b - p_a;)
         if (stop) break;
+        WPROF(++p_np;)
         const int lag = (a.tspec && !a.exact_only)
                             ? walk_preamble_fft(a, hit, big, P, tw_m, scr, best, unsure, xs, E, normv, t)
                             : walk_preamble(a, hit, xs, ctap, E, normv, best, unsure, mred, t);
+        WPROF(p_pre += clock64() - p_b;)
         const long pb = (lag == INT_MAX ? -10 : hit + lag) + 1;  // rx.cpp:160
         if (pb < -2) {                                            // rx.cpp:162-168
             pos = hit + a.msg;
@@ -1342,6 +1400,11 @@ __global__ void __launch_bounds__(WALK_THREADS, 4) stream_walk_kernel(WalkArgs a
             if (ncore == 0) first_in = nrec;
             ++ncore;
         }
+        past = pb >= end;
+        // a frame of the next core located from a state before this core's
+        // end: that state is the hand-over (a re-walk from pb + msg would
+        // miss the frame)
+        if (past && exitp < 0) exitp = spos;
         ++nrec;
         pos = pb + a.msg;  // rx.cpp:192
     }
@@ -1353,6 +1416,12 @@ __global__ void __launch_bounds__(WALK_THREADS, 4) stream_walk_kernel(WalkArgs a
             a.first_in[c] = first_in;
         }
     }
+    }  // chunks
+    WPROF(if (t0 == 0 && blockIdx.x < 8192) {
+        unsigned long long* q = g_walk_prof + 8 * blockIdx.x;
+        q[0] = clock64() - p_c0; q[1] = p_t2; q[2] = p_n2; q[3] = p_pre; q[4] = p_np;
+        q[5] = p_steps; q[6] = p_w0; q[7] = wall_clock64();
+    })
 }
 
 __global__ void gather_kernel(GatherArgs a)
@@ -1497,3 +1566,17 @@ hipError_t launch_gather(const GatherArgs& a, hipStream_t st)
 }
 
 }  // namespace ofdm
+
+#ifdef OFDM_WALK_PROF
+extern "C" int ofdm_walk_prof(unsigned long long* out, unsigned long long* fallbacks)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ofdm::g_walk_prof), sizeof(unsigned long long) * 8192 * 8) != hipSuccess)
+        return -1;
+    if (hipMemcpyFromSymbol(fallbacks, HIP_SYMBOL(ofdm::g_walk_fallbacks), sizeof(unsigned long long)) != hipSuccess)
+        return -1;
+    if (hipMemcpyFromSymbol(out + 8192 * 8, HIP_SYMBOL(ofdm::g_walk_sub), sizeof(unsigned long long) * 8192 * 8) !=
+        hipSuccess)
+        return -1;
+    return 0;
+}
+#endif

@@ -86,8 +86,11 @@ struct WalkArgs {
     double pr_level;
     long pre, msg;              // preamble / message lengths (samples)
     long chunk, halo;           // core samples per chunk; walk-in before the core
+    long ext;                   // walk-on past the core end while looking for the first frame there
     const int* chunk_ids;       // nullable: chunk of each workgroup (re-walk launches)
     const long* start_pos;      // nullable: exact start state per workgroup (re-walk)
+    int* queue;                 // nullable: chunk counter (zeroed) the workgroups take chunks from until
+    long nchunks;               //   nchunks are taken (dynamic balance); else one chunk per workgroup
     int max_rec;                // records per chunk
     long* rec;                  // [chunk][max_rec] preamble starts found
     int* nrec;                  // [chunk] frames found (> max_rec: overflow)

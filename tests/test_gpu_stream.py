@@ -98,6 +98,18 @@ def test_stream_config4_matches_sequential_walk(chunk):
     assert len(want) >= 20  # the grid-relative T2 search misses some frames, as the reference does
 
 
+@pytest.mark.parametrize("halo,ext", [(0, 0), (100, 0), (250, 0), (500, 0), (100, 2000), (1500, 2000)])
+@pytest.mark.parametrize("chunk", [0, 9000, 20000])
+def test_stream_short_halo_rewalks_match_sequential_walk(monkeypatch, halo, ext, chunk):
+    # walk-in halos (in 1/1000 frames) too short to meet the true walk force
+    # re-walks from the previous chunk's hand-over state (with or without the
+    # walk-on past the core end): still exact
+    monkeypatch.setenv("OFDM_WALK_HALO", str(halo))
+    monkeypatch.setenv("OFDM_WALK_EXT", str(ext))
+    x, data = impaired_stream(D, 40, seed=4)
+    check_against_oracle(D, x, run_stream(D, x, chunk=chunk))
+
+
 def test_stream_walk_certified_search_equals_serial_recurrence(monkeypatch):
     # the walker's parallel preamble search (window sums + error bound) against
     # the reference's serial running-energy recurrence, forced by the test hook
