@@ -33,6 +33,13 @@
 #pragma clang fp contract(off)
 
 namespace ofdm {
+#ifdef OFDM_WALK_PROF  // timing experiment only: stream_params_kernel phase clocks (summed over frames)
+__device__ unsigned long long g_params_prof[16];
+#define PPROF(...) __VA_ARGS__
+#else
+#define PPROF(...)
+#endif
+
 
 namespace {
 
@@ -742,6 +749,22 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamPa
     const double cfo = a.cfo[f];
     const int L = N + a.cp, half = a.D / 2, Q = 1 + a.S, LT = L / T, CT = a.cp / T;
 
+    PPROF(unsigned long long pc0 = clock64(), pc1;)
+    // The per-thread table entries are requested before the stream samples:
+    // vector-memory returns are in order, so a table load issued later waits
+    // behind every stream load in flight on the CU. (Doing the same for the
+    // preamble template, through LDS, costs more occupancy than it saves:
+    // params 230 -> 263 us.)
+    int dbin[2], dslot[2];
+    double2 mpre[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int i = t + T * u;
+        dbin[u] = i < half ? a.tab.data_bin[i] : 0;
+        dslot[u] = i < half ? a.tab.data_slot[i] : 0;
+        mpre[u] = i < half ? a.mod_pre[i] : make_double2(1.0, 0.0);
+    }
+    const int pbin = t < a.P ? a.tab.pilot_bin[t] : 0;
     // the preamble form into registers, then the message symbols' CP pairs
     double2 z[RMAX];
 #pragma unroll
@@ -789,6 +812,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamPa
         if (two) wave_part(q + 1, acc1);
     }
     __syncthreads();
+    PPROF(pc1 = clock64(); if (t == 0) atomicAdd(&g_params_prof[0], pc1 - pc0); pc0 = pc1;)
     for (int q = t; q < Q; q += T) {
         double2 acc = make_double2(0.0, 0.0);
         for (int u = 0; u < NWV; ++u) acc = cadd(acc, part[q * NWV + u]);
@@ -796,6 +820,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamPa
         phi[q] = atan2(r.y, r.x);
     }
     __syncthreads();
+    PPROF(pc1 = clock64(); if (t == 0) atomicAdd(&g_params_prof[1], pc1 - pc0); pc0 = pc1;)
     if (t == 0) {
         double acc = 0.0;
         for (int q = 0; q < Q; ++q) {
@@ -825,6 +850,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamPa
         if (t == 0) phpr = atan2(acc.y, acc.x);
         __syncthreads();
     }
+    PPROF(pc1 = clock64(); if (t == 0) atomicAdd(&g_params_prof[2], pc1 - pc0); pc0 = pc1;)
     const double phr = phpr;
 
     // chan_char_lq: FFT_FORM::read of the corrected preamble symbol
@@ -843,30 +869,39 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamPa
         for (int i = 0; i < 8; ++i) v[i] = cmul_exact(fftb[t + T * i], rot);
         lds_barrier();
         fft_block<LOGN, -1>(v, t, lds_tw, fftb);
-        for (int j = t; j < a.P; j += T) pil[j] = fftb[lds_swz(a.tab.pilot_bin[j])];
-        for (int i = t; i < half; i += T) dat[i] = fftb[lds_swz(a.tab.data_bin[i])];
+        if (t < a.P) pil[t] = fftb[lds_swz(pbin)];  // P <= T (host-checked)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)  // D/2 <= 2T (host-checked)
+            if (t + T * u < half) dat[t + T * u] = fftb[lds_swz(dbin[u])];
     }
     __syncthreads();
+    PPROF(pc1 = clock64(); if (t == 0) atomicAdd(&g_params_prof[3], pc1 - pc0); pc0 = pc1;)
     double acc = 0.0;
     for (int i = t; i < a.P; i += T) acc += hypot(pil[i].x, pil[i].y);
     acc = block_sum2<T>(make_double2(acc, 0.0), red).x;
     const double phys = acc / ((double)a.P * a.pilot_ampl);
-    for (int i = t; i < half; i += T) {
-        const int j = a.tab.data_slot[i];
-        const double2 p0 = make_double2(pil[j].x / phys, pil[j].y / phys);
-        const double2 coef = cdiv_exact(p0, p0);
-        const double2 fs = make_double2(dat[i].x / phys, dat[i].y / phys);
-        const double2 q = cdiv_exact(cdiv_exact(fs, coef), a.mod_pre[i]);
-        ph[i] = atan2(q.y, q.x);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int i = t + T * u;
+        if (i < half) {
+            const int j = dslot[u];
+            const double2 p0 = make_double2(pil[j].x / phys, pil[j].y / phys);
+            const double2 coef = cdiv_exact(p0, p0);
+            const double2 fs = make_double2(dat[i].x / phys, dat[i].y / phys);
+            const double2 q = cdiv_exact(cdiv_exact(fs, coef), mpre[u]);
+            ph[i] = atan2(q.y, q.x);
+        }
     }
     __syncthreads();
     unwrap_scan<T>(ph, half, reinterpret_cast<unsigned*>(red + 24));  // one-pass unwrap (Frame.hpp:407-414)
+    PPROF(pc1 = clock64(); if (t == 0) atomicAdd(&g_params_prof[4], pc1 - pc0); pc0 = pc1;)
     double sxy = 0.0, sy = 0.0;
     for (int i = t; i < half; i += T) {
         sxy += ph[i] * i;
         sy += ph[i];
     }
     const double2 sums = block_sum2<T>(make_double2(sxy, sy), red + 16);
+    PPROF(pc1 = clock64(); if (t == 0) atomicAdd(&g_params_prof[5], pc1 - pc0); pc0 = pc1;)
     const double hn = (double)half;
     const double sx = hn * (hn - 1) / 2, sx2 = (hn - 1) * hn * (2 * hn - 1) / 6;
     const double b = (sums.x - sx * sums.y) / (sx2 - sx * sx);
@@ -884,6 +919,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamPa
         // constell /= chan would round it) instead of a division per point
         chan[i] = a.chan_recip ? cdiv_exact(make_double2(1.0, 0.0), make_double2(cs, sn)) : make_double2(cs, sn);
     }
+    PPROF(pc1 = clock64(); if (t == 0) atomicAdd(&g_params_prof[6], pc1 - pc0); pc0 = pc1;)
     // message symbols: theta(m) = A_s + B_s m over the CP-stripped body
     for (int s = t; s < a.S; s += T) {
         const int q = 1 + s;
@@ -897,6 +933,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamPa
         o[2] = cs;
         o[3] = sn;
     }
+    PPROF(pc1 = clock64(); if (t == 0) { atomicAdd(&g_params_prof[7], pc1 - pc0); atomicAdd(&g_params_prof[8], 1ULL); })
 }
 
 template <int LOGN>
@@ -1575,6 +1612,9 @@ extern "C" int ofdm_walk_prof(unsigned long long* out, unsigned long long* fallb
     if (hipMemcpyFromSymbol(fallbacks, HIP_SYMBOL(ofdm::g_walk_fallbacks), sizeof(unsigned long long)) != hipSuccess)
         return -1;
     if (hipMemcpyFromSymbol(out + 8192 * 8, HIP_SYMBOL(ofdm::g_walk_sub), sizeof(unsigned long long) * 8192 * 8) !=
+        hipSuccess)
+        return -1;
+    if (hipMemcpyFromSymbol(out + 2 * 8192 * 8, HIP_SYMBOL(ofdm::g_params_prof), sizeof(unsigned long long) * 16) !=
         hipSuccess)
         return -1;
     return 0;

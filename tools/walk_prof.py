@@ -19,11 +19,11 @@ import ofdm_mi355x as M  # noqa: E402
 sys.argv = [sys.argv[0], "--reps", "1"] + sys.argv[1:]
 stream_bench.main()
 lib = M.lib()
-buf = np.zeros(2 * 8192 * 8, dtype=np.uint64)
+buf = np.zeros(2 * 8192 * 8 + 16, dtype=np.uint64)
 fb = np.zeros(1, dtype=np.uint64)
 assert lib.ofdm_walk_prof(buf.ctypes.data_as(C.c_void_p), fb.ctypes.data_as(C.c_void_p)) == 0
 q = buf[:8192 * 8].reshape(8192, 8).astype(np.float64)
-sub = buf[8192 * 8:].reshape(8192, 8).astype(np.float64)
+sub = buf[8192 * 8:2 * 8192 * 8].reshape(8192, 8).astype(np.float64)
 live = q[:, 5] > 0
 q = q[live]
 sub = sub[live]
@@ -45,6 +45,9 @@ res = {
     "corr_wall_steps": float(np.corrcoef(wall_us, steps)[0, 1]),
     "corr_wall_t2iters": float(np.corrcoef(wall_us, n2)[0, 1]),
     "corr_wall_cycles": float(np.corrcoef(wall_us, tot)[0, 1]),
+    # stream_params_kernel phases, cycles per frame (thread 0): CP sums, symbol phases,
+    # preamble correction, FFT, pilot/bin phases (4: incl. unwrap), sums, channel, ramps
+    "params_phases": [round(float(x) / max(float(buf[-16 + 8]), 1.0), 1) for x in buf[-16:-8]],
     "cyc_per_us_min_max": [float((tot / wall_us).min()), float((tot / wall_us).max())],
 }
 np.savez(os.path.join("gpurun_out", "wprof%s.npz" % ("_i16" if "--i16" in sys.argv else "")), q=q, sub=sub)
