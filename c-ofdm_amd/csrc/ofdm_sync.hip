@@ -379,6 +379,22 @@ __global__ void __launch_bounds__(G * (1 << LOGM) / 8) cfo_kernel(CfoArgs a)
     const long f = blockIdx.x;
     if (a.count && f >= *a.count) return;  // uniform: past the speculative frame count
     const long x0 = a.starts ? a.starts[f] : f * a.frame_stride;
+    // the combine twiddles are requested before the samples (in-order
+    // vector-memory returns: issued after them they would wait behind every
+    // stream load in flight on the CU; cfo 93 -> 80 us on config 4)
+    constexpr int KM = (M + NT - 1) / NT;
+    double2 twk[KM][G > 1 ? G - 1 : 1], twg[G > 1 ? G - 1 : 1];
+    if constexpr (G > 1) {
+#pragma unroll
+        for (int u = 0; u < KM; ++u)
+#pragma unroll
+            for (int q = 1; q < G; ++q) {
+                const int k = tid + NT * u;
+                twk[u][q - 1] = k < M ? a.tw_full[(long)q * k % S] : make_double2(1.0, 0.0);
+            }
+#pragma unroll
+        for (int q = 1; q < G; ++q) twg[q - 1] = a.tw_full[(long)q * M];
+    }
     load_twiddles<LOGM>(a.tw_sub, lds_tw, tid, NT);
     double2 v[8];
 #pragma unroll
@@ -396,7 +412,10 @@ __global__ void __launch_bounds__(G * (1 << LOGM) / 8) cfo_kernel(CfoArgs a)
     // X[k + M*r] = sum_q W_S^{q k} W_G^{q r} F_q[k]; amp stored fftshifted:
     // shifted[i] = spec[(i + S/2) % S]  (Frame.hpp:300-305)
     const int half = S / 2;
-    for (int k = tid; k < M; k += NT) {
+#pragma unroll
+    for (int u = 0; u < KM; ++u) {
+        const int k = tid + NT * u;
+        if (k >= M) break;
         if constexpr (G == 1) {
             const double2 z = fftb[lds_swz(k)];
             amp[(k + half) % S] = hypot(z.x, z.y);
@@ -405,13 +424,14 @@ __global__ void __launch_bounds__(G * (1 << LOGM) / 8) cfo_kernel(CfoArgs a)
 #pragma unroll
             for (int q = 0; q < G; ++q) {
                 const double2 fq = fftb[q * M + lds_swz(k)];
-                tq[q] = q == 0 ? fq : cmul(fq, a.tw_full[(long)q * k % S]);
+                tq[q] = q == 0 ? fq : cmul(fq, twk[u][q - 1]);
             }
 #pragma unroll
             for (int r = 0; r < G; ++r) {
                 double2 acc = tq[0];
 #pragma unroll
-                for (int q = 1; q < G; ++q) acc = cadd(acc, cmul(tq[q], a.tw_full[(long)((q * r) % G) * M]));
+                for (int q = 1; q < G; ++q)
+                    acc = cadd(acc, cmul(tq[q], (q * r) % G ? twg[(q * r) % G - 1] : make_double2(1.0, 0.0)));
                 const int idx = k + M * r;
                 amp[(idx + half) % S] = hypot(acc.x, acc.y);
             }
@@ -419,21 +439,38 @@ __global__ void __launch_bounds__(G * (1 << LOGM) / 8) cfo_kernel(CfoArgs a)
     }
     __syncthreads();
     // first argmax inside each pilot window [borders[i], borders[i+1]), i != P/2
-    // (std::max_element: strictly-greater keeps the first maximum); one
-    // thread per window, windows are ~41 bins wide.
-    for (int i = tid; i <= a.P; i += NT) {
-        const int lo = a.borders[i], hi = a.borders[i + 1];
-        int bi = hi;  // max_element of an empty range = end
-        if (lo < hi) {
-            bi = lo;
-            double bv = amp[lo];
-            for (int j = lo + 1; j < hi; ++j)
-                if (bv < amp[j]) {
-                    bv = amp[j];
-                    bi = j;
-                }
+    // (std::max_element: strictly-greater keeps the first maximum). A group
+    // of AG lanes per window: each lane the first maximum of its strided
+    // share, then a butterfly keeping the larger value, the lower index on
+    // ties, which is the window's first maximum.
+    constexpr int AG = 8;
+    for (int i0 = 0; i0 <= a.P; i0 += NT / AG) {
+        const int i = i0 + tid / AG, l = tid % AG;
+        const bool act = tid < (NT / AG) * AG && i <= a.P;
+        int lo = 0, hi = 0;
+        if (act) {
+            lo = a.borders[i];
+            hi = a.borders[i + 1];
         }
-        wsum[i] = bi;
+        double bv = -1.0;  // below every magnitude
+        int bi = INT_MAX;
+        for (int j = lo + l; j < hi; j += AG)
+            if (bv < amp[j]) {
+                bv = amp[j];
+                bi = j;
+            }
+#pragma unroll
+        for (int o = 1; o < AG; o <<= 1) {  // AG-lane groups are aligned within a wave
+            const double ov = __shfl_xor(bv, o);
+            const int oi = __shfl_xor(bi, o);
+            if (ov > bv || (ov == bv && oi < bi)) {
+                bv = ov;
+                bi = oi;
+            }
+        }
+        // max_element of an empty range = end; a NaN first element is kept
+        // (nothing compares greater than it)
+        if (act && l == 0) wsum[i] = lo < hi ? (isnan(amp[lo]) ? lo : bi) : hi;
     }
     __syncthreads();
     if (tid == 0) {
