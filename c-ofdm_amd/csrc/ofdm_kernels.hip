@@ -492,6 +492,35 @@ __device__ __forceinline__ void dma_symbol(const RxArgs& a, long off, void* stag
     }
 }
 
+// LDS-DMA of a frame's D channel carriers (complex<double>) to chl: RX_DPT
+// 16-B transfers per lane at most, lanes past D masked off. Issued before the
+// next frame's symbol-0 DMA, so (returns are in order) they land first.
+template <int LOGN>
+__device__ __forceinline__ void dma_chan(const double2* chan, int D, double2* chl, int t)
+{
+    constexpr int T = (1 << LOGN) / 8;
+    const int w0 = t & ~63;
+#pragma unroll
+    for (int i = 0; i < RX_DPT; ++i) {
+        const int e0 = w0 + T * i;  // wave-uniform
+        if (e0 + (t & 63) < D) {
+            const char* g = reinterpret_cast<const char*>(chan + e0 + (t & 63));
+            const unsigned lds = __builtin_amdgcn_readfirstlane(
+                (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)((char*)chl + (size_t)e0 * 16));
+            unsigned keep;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\t"
+                "s_mov_b32 m0, %2\n\t"
+                "s_nop 0\n\t"
+                "global_load_lds_dwordx4 %1, off\n\t"
+                "s_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(g), "s"(lds)
+                : "memory");
+        }
+    }
+}
+
 template <int LOGN, bool I16>
 __device__ __forceinline__ double2 stage_get(const void* stage, int e)
 {
@@ -655,7 +684,16 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
             }
         }
         lds_barrier();  // pilots of the last symbol visible; every thread is done reading bufB
-        if (fl + fstep < nfr) dma_symbol<LOGN, I16>(a, body0(frame_of(fl + fstep)), bufB, t);
+        // The channel carriers go to LDS (bufA past the decisions) by DMA
+        // issued ahead of the next frame's symbol 0: read per point from HBM
+        // behind that DMA (in-order returns), they cost the stream rx ~18%.
+        const double2* chan = a.chan ? a.chan + f * a.chan_stride : nullptr;
+        const int dec_b = (S * D + 15) & ~15;
+        double2* chl = reinterpret_cast<double2*>(reinterpret_cast<char*>(bufA) + dec_b);
+        const bool chan_lds = chan && dec_b + D * 16 <= N * 16;  // uniform
+        if (chan_lds) dma_chan<LOGN>(chan, D, chl, t);
+        const bool next = fl + fstep < nfr;
+        if (next) dma_symbol<LOGN, I16>(a, body0(frame_of(fl + fstep)), bufB, t);
 
         // phys_pilot_ampl = sum |pilot| / (P*S*pilot_ampl)   (Frame.cpp:76-80)
         double acc = 0.0;
@@ -672,16 +710,28 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
             const double2 g = cdiv_exact(make_double2(1.0, 0.0), coef);
             gain[i] = make_double2(g.x / phys, g.y / phys);
         }
+        if (chan_lds) {  // the channel DMA landed (the 8 symbol-0 transfers may still fly)
+            if (next)
+                asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         lds_barrier();
 
-        const double2* chan = a.chan ? a.chan + f * a.chan_stride : nullptr;
         auto emit = [&](int s, int i, double2 yv) {
             // opaque: the per-point addresses are computed here, not hoisted
             // out of the emit loop and held (32 of them) across it
             int d = t + T * i, gi = s * P + (pk[i] >> 16);
             asm volatile("" : "+v"(d), "+v"(gi));
             double2 o = cmul_exact(yv, gain[gi]);
-            if (chan) o = a.chan_recip ? cmul_exact(o, chan[d]) : cdiv_exact(o, chan[d]);
+#ifdef OFDM_RX_NOCHAN  // timing experiment only: no channel correction
+            (void)chan;
+#else
+            if (chan) {
+                const double2 cv = chan_lds ? chl[d] : chan[d];
+                o = a.chan_recip ? cmul_exact(o, cv) : cdiv_exact(o, cv);
+            }
+#endif
             if (a.constell) store_nt(a.constell + (f * S + s) * D + d, o);
             dec[whole_frame_dec ? s * D + d : d] = (uint8_t)decide(o, a.k, s1, m);
         };
