@@ -158,6 +158,8 @@ struct ofdm_ctx {
     hipStream_t h_frames_stream = nullptr;  // stream of the last copy out of h_frames
     bool h_frames_used = false;
     hipEvent_t ev_walk = nullptr;  // walk records landed in h_walk
+    hipEvent_t ev_wdone = nullptr;  // the walk kernel finished (caller's stream)
+    hipStream_t side = nullptr;     // copies the walk records out beside the decode
 
     ofdm::DevTables tables(bool bpsk) const
     {
@@ -306,6 +308,8 @@ int ofdm_destroy(ofdm_ctx* c)
     for (auto* g : {&c->h_walk, &c->h_frames})
         if (g->p) (void)hipHostFree(g->p);
     if (c->ev_walk) (void)hipEventDestroy(c->ev_walk);
+    if (c->ev_wdone) (void)hipEventDestroy(c->ev_wdone);
+    if (c->side) (void)hipStreamDestroy(c->side);
     for (auto& pl : c->cfo_plans) {
         if (pl.tw_sub) (void)hipFree(pl.tw_sub);
         if (pl.tw_full) (void)hipFree(pl.tw_full);
@@ -1306,9 +1310,15 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     long* rec = reinterpret_cast<long*>(hb);
     long* ex = reinterpret_cast<long*>(hb + rec_b);
     int* nrec = reinterpret_cast<int*>(ex + nchunks + 2);
-    HIP_TRY(hipMemcpyAsync(hb, wb, walk_b, hipMemcpyDeviceToHost, st));
+    // the copy runs on a side stream, so the compaction and the decode on the
+    // caller's stream do not queue behind it
     if (!c->ev_walk) HIP_TRY(hipEventCreateWithFlags(&c->ev_walk, hipEventDisableTiming));
-    HIP_TRY(hipEventRecord(c->ev_walk, st));
+    if (!c->ev_wdone) HIP_TRY(hipEventCreateWithFlags(&c->ev_wdone, hipEventDisableTiming));
+    if (!c->side) HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    HIP_TRY(hipEventRecord(c->ev_wdone, st));
+    HIP_TRY(hipStreamWaitEvent(c->side, c->ev_wdone, 0));
+    HIP_TRY(hipMemcpyAsync(hb, wb, walk_b, hipMemcpyDeviceToHost, c->side));
+    HIP_TRY(hipEventRecord(c->ev_walk, c->side));
     // Speculative decode: every chunk's in-core records, compacted on the
     // device behind the copy of the walk records, are decoded while the host
     // stitches the walks. That list is the stitched walk unless a chunk needs
