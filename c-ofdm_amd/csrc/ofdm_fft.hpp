@@ -298,6 +298,14 @@ __device__ __forceinline__ void stockham_pass(double2 (&v)[8], int t, const doub
     stockham_apply<LOGN, R, NS, SIGN>(v, t, pass_twiddles<LOGN, R, NS, SIGN>(t, lds_tw), lds);
 }
 
+// Last pass kept in registers (v[i] = X[t + T*i] on exit; see fft_regs).
+template <int LOGN, int R, int NS, int SIGN>
+__device__ __forceinline__ void stockham_pass_regs(double2 (&v)[8], int t, const double2* __restrict__ lds_tw,
+                                                   double2* __restrict__ lds)
+{
+    stockham_apply<LOGN, R, NS, SIGN, false>(v, t, pass_twiddles<LOGN, R, NS, SIGN>(t, lds_tw), lds);
+}
+
 template <int LOGN>
 __device__ __forceinline__ void lds_load8(double2 (&v)[8], int t, const double2* __restrict__ lds)
 {
@@ -410,6 +418,38 @@ __device__ __forceinline__ void fft_regs(double2 (&v)[8], int t, const double2* 
     static_assert(LOGN >= 6 && LOGN <= 12, "N must be 64..4096");
     stockham_pass<LOGN, 8, 1, SIGN>(v, t, lds_tw, lds);
     fft_regs_tail<LOGN, 1, SIGN>(v, t, lds_tw, lds);
+}
+
+// fft_regs run by the first N/8 threads of a larger workgroup (`active`
+// wave-uniform); every thread takes the barriers.
+template <int LOGN, int PASS, int SIGN>
+__device__ __forceinline__ void fft_regs_tail_active(double2 (&v)[8], int t, const double2* __restrict__ lds_tw,
+                                                     double2* __restrict__ lds, bool active)
+{
+    using S = FftShape<LOGN>;
+    constexpr int NPASS = S::NPASS8 + (S::REM ? 1 : 0);
+    constexpr bool is8 = PASS < S::NPASS8;
+    constexpr int R = is8 ? 8 : (1 << S::REM);
+    constexpr int NS = 1 << (3 * PASS);
+    constexpr bool LAST = PASS == NPASS - 1;
+    lds_barrier();  // previous pass fully written
+    if (active) lds_load8<LOGN>(v, t, lds);
+    if constexpr (LAST) {
+        if (active) stockham_pass_regs<LOGN, R, NS, SIGN>(v, t, lds_tw, lds);
+    } else {
+        lds_barrier();  // everyone has read before the image is overwritten
+        if (active) stockham_pass<LOGN, R, NS, SIGN>(v, t, lds_tw, lds);
+        fft_regs_tail_active<LOGN, PASS + 1, SIGN>(v, t, lds_tw, lds, active);
+    }
+}
+
+template <int LOGN, int SIGN>
+__device__ __forceinline__ void fft_regs_active(double2 (&v)[8], int t, const double2* __restrict__ lds_tw,
+                                                double2* __restrict__ lds, bool active)
+{
+    static_assert(LOGN >= 9 && LOGN <= 12, "N/8 must be whole waves");
+    if (active) stockham_pass<LOGN, 8, 1, SIGN>(v, t, lds_tw, lds);
+    fft_regs_tail_active<LOGN, 1, SIGN>(v, t, lds_tw, lds, active);
 }
 
 // ---------------------------------------------------------------- ping-pong

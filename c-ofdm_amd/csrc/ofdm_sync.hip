@@ -1228,7 +1228,8 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
         *best = INT_MAX;
         *unsure = INT_MAX;
     }
-    fft_block_active<LM, -1>(v, t, tw_m, buf, active);  // X (barriers: P and scr visible)
+    // X, its last pass in registers: v[i] = X[t + TM*i] (barriers: P and scr visible)
+    fft_regs_active<LM, -1>(v, t, tw_m, buf, active);
     WPROF(const unsigned long long q1 = clock64();)
 
     // inclusive prefix sums of P: thread t owns R consecutive entries
@@ -1249,9 +1250,9 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const int k = t + TM * i;
-        if (active) v[i] = cmul(buf[lds_swz(k)], a.tspec[k]);
+        if (active) v[i] = cmul(v[i], a.tspec[k]);
     }
-    lds_barrier();  // every thread has read X and the wave totals are visible
+    lds_barrier();  // the wave totals are visible; every thread is done with the forward image
     double run = inc - loc;
     for (int w = 0; w < (t >> 6); ++w) run += scr[8 + w];
     for (int r = 0; r < R; ++r) {
@@ -1411,13 +1412,16 @@ __global__ void __launch_bounds__(WALK_THREADS, 4) stream_walk_kernel(WalkArgs a
 #pragma unroll
             for (int i = 0; i < 8; ++i) v[i] = live ? stream_sample(a, b + tt + T * i) : make_double2(0.0, 0.0);
             WPROF(const unsigned long long r0 = clock64();)
-            fft_block<LOGT, -1>(v, tt, lds_tw, fftb + g * N);
+            // the last pass stays in registers: v[i] = X[tt + T*i], the bins
+            // this thread sums (no final LDS write, barrier and re-read); the
+            // image is next written after the bestg barriers below
+            fft_regs<LOGT, -1>(v, tt, lds_tw, fftb + g * N);
             WPROF(const unsigned long long r1 = clock64();)
             double tot = 0.0, sine = 0.0;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const int k = tt + T * i;
-                const double2 z = fftb[g * N + lds_swz(k)];
+                const double2 z = v[i];
                 const double e = z.x * z.x + z.y * z.y;
                 const double m = (double)((k >= a.a1 && k <= a.b1) + (k >= a.a2 && k <= a.b2));
                 tot += e;
