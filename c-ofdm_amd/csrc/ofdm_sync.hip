@@ -1282,6 +1282,7 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
     const double scan_err = (4.0 * R + 64.0) * U * ptot;
     const double ef = 1024.0 * U * sqrt(ptot * 1.0625) * a.tspec_max;
     constexpr double inv_m = 1.0 / M;
+    const double lev2 = a.pr_level * a.pr_level;
     for (int i = t; i < C; i += WALK_THREADS) {
         const double sn = P[i + L - 1] - (i ? P[i - 1] : 0.0);
         const double2 e = buf[lds_swz(i)];
@@ -1290,13 +1291,17 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
         if (sn + B <= 1.0) {
             d = 0;  // n_i <= 1 for sure
         } else {
-            const double ae = hypot(e.x, e.y) * inv_m;
-            const double r_hi = (ae + ef) / sqrt(fmax(sn - B, 0x1.0p-1000)) * (1.0 + 16.0 * U);
-            const double r_lo = (ae - ef) / sqrt(sn + B) * (1.0 - 16.0 * U);
-            if (r_hi <= a.pr_level)
+            // the ratio tests squared (one sqrt, no hypot or division): the
+            // 32U / 16U slack factors cover these roundings and the
+            // reference's own (hypot, sqrt, divide), so a certain FAIL / PASS
+            // is still one the reference makes (see the bound above)
+            const double ae = sqrt(e.x * e.x + e.y * e.y) * inv_m;
+            const double hi = (ae + ef) * (1.0 + 32.0 * U);
+            const double lo = fmax(ae - ef, 0.0) * (1.0 - 32.0 * U);
+            if (hi * hi <= lev2 * fmax(sn - B, 0x1.0p-1000) * (1.0 - 16.0 * U))
                 d = 0;
             else
-                d = (sn - B > 1.0 && r_lo > a.pr_level) ? 1 : 2;
+                d = (sn - B > 1.0 && lo * lo > lev2 * (sn + B) * (1.0 + 16.0 * U)) ? 1 : 2;
         }
         if (d) atomicMin(best, i);
         if (d == 2) atomicMin(unsure, i);
