@@ -1048,6 +1048,17 @@ __device__ __forceinline__ double2 stream_sample(const A& a, long j)
     return a.iq[j];
 }
 
+// The same for j known to lie in [0, n) (no per-sample 64-bit bounds test).
+template <class A>
+__device__ __forceinline__ double2 stream_sample_in(const A& a, long j)
+{
+    if (a.iq16) {
+        const short2 v = a.iq16[j];
+        return make_double2((double)v.x, (double)v.y);
+    }
+    return a.iq[j];
+}
+
 // PREAMBLE_FORM::find_preamble from s: first lag with norm > 1 and
 // |sum_j x[s+i+j] c_j| / sqrt(norm) > level (Frame.cpp:338-378), INT_MAX if
 // none. Exact form: the running energy is the reference's serial recurrence
@@ -1207,6 +1218,7 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
     constexpr int LM = WALK_FFT_LOGM, M = WALK_FFT_M, TM = M / 8;
     const int L = a.L, C = a.cycles, W = C + L;
     const bool active = t < TM;
+    const bool whole = s >= 0 && s + W <= a.n;  // uniform: the window needs no bounds tests
     WPROF(const unsigned long long q0 = clock64();)
     double2 v[8];
     double emax = 0.0;
@@ -1215,7 +1227,7 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
         const int k = t + TM * i;
         v[i] = make_double2(0.0, 0.0);
         if (active && k < W) {
-            v[i] = stream_sample(a, s + k);
+            v[i] = whole ? stream_sample_in(a, s + k) : stream_sample(a, s + k);
             const double e2 = add_rn(mul_rn(v[i].x, v[i].x), mul_rn(v[i].y, v[i].y));
             P[k] = e2;
             emax = fmax(emax, e2);
@@ -1415,7 +1427,7 @@ __global__ void __launch_bounds__(WALK_THREADS, 4) stream_walk_kernel(WalkArgs a
             const bool live = b + N <= a.n;
             double2 v[8];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) v[i] = live ? stream_sample(a, b + tt + T * i) : make_double2(0.0, 0.0);
+            for (int i = 0; i < 8; ++i) v[i] = live ? stream_sample_in(a, b + tt + T * i) : make_double2(0.0, 0.0);
             WPROF(const unsigned long long r0 = clock64();)
             // the last pass stays in registers: v[i] = X[tt + T*i], the bins
             // this thread sums (no final LDS write, barrier and re-read); the
