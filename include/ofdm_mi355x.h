@@ -289,7 +289,9 @@ int ofdm_sync_frames(ofdm_ctx* ctx, double* frames, size_t nframes, size_t frame
  * pb_out[f] preamble start, bytes_out (bytes_per_frame per frame),
  * constell_out (D*num_symb complex per frame), cfo_out. *nframes_out = frames
  * found; outputs hold the first max_frames. The input is not modified.
- * Synchronises `stream` (the host stitches the walk). */
+ * Returns once the host has stitched the walk (it waits for the walk records);
+ * the decode is enqueued on `stream` and may still be running, so order later
+ * work on `stream`, or synchronise it, before reading the outputs. */
 int ofdm_rx_stream(ofdm_ctx* ctx, const double* iq, size_t n, size_t max_frames, long chunk,
                    long* pb_out, uint8_t* bytes_out, double* constell_out, double* cfo_out,
                    size_t* nframes_out, void* stream);
