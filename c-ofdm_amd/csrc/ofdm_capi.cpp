@@ -1227,6 +1227,7 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     ofdm_ctx::CfoPlan* pl = nullptr;
     const bool fused = c->S <= ofdm::RX_SMAX && c->D <= ofdm::RX_DPT * (c->N / 8) && c->P <= c->N / 8 &&
                        c->npr == 1 && c->S + 1 <= 64 && c->L % (c->N / 8) == 0 && c->L / (c->N / 8) <= 16 &&
+                       c->cp <= 2 * (c->N / 8) &&  // stream_params_kernel: CP template in 2 registers
                        cfo_plan(c, c->npr, &pl) == OFDM_OK;
     const size_t per = (size_t)c->D * sizeof(double2) + (size_t)c->S * 4 * sizeof(double) + sizeof(double);
     const long npts = (long)c->D * c->S;

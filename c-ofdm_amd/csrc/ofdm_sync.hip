@@ -761,7 +761,7 @@ __device__ __forceinline__ double2 src_sample(const double2* iq, const short2* i
 }  // namespace
 
 template <int LOGN>
-__global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamParamsArgs a)
+__global__ void __launch_bounds__((1 << LOGN) / 8, 3) stream_params_kernel(StreamParamsArgs a)
 {
     // one preamble symbol (npr == 1) whose form length L is a multiple of T
     // (host-checked): thread t holds the preamble form samples t + T*r, r < L/T
@@ -792,14 +792,20 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamPa
     // behind every stream load in flight on the CU. (Doing the same for the
     // preamble template, through LDS, costs more occupancy than it saves:
     // params 230 -> 263 us.)
-    int dbin[2], dslot[2];
-    double2 mpre[2];
+    // data carrier i = t + T*u (D <= 4T, host-checked): its bin and BPSK
+    // preamble point; the slot for the first half (chan_char_lq); the CP part
+    // of the preamble template (pr_phase_sinh's time-domain share)
+    int dbin[4], dslot[2];
+    double2 mpre[4], prc[2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < 4; ++u) {
         const int i = t + T * u;
-        dbin[u] = i < half ? a.tab.data_bin[i] : 0;
-        dslot[u] = i < half ? a.tab.data_slot[i] : 0;
-        mpre[u] = i < half ? a.mod_pre[i] : make_double2(1.0, 0.0);
+        dbin[u] = i < a.D ? a.tab.data_bin[i] : 0;
+        mpre[u] = i < a.D ? a.mod_pre[i] : make_double2(0.0, 0.0);
+        if (u < 2) {
+            dslot[u] = i < half ? a.tab.data_slot[i] : 0;
+            prc[u] = u < CT ? a.pre[i] : make_double2(0.0, 0.0);  // CT <= 2 (host-checked)
+        }
     }
     const int pbin = t < a.P ? a.tab.pilot_bin[t] : 0;
     // the preamble form into registers, then the message symbols' CP pairs
@@ -866,8 +872,15 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamPa
         }
     }
     // freq_shift + cp_freq_sinh on the preamble: theta(j) = slope * j (psi_0 = 0),
-    // applied as e^{i slope t} * (e^{i slope T})^r
+    // applied as e^{i slope t} * (e^{i slope T})^r. pr_phase_sinh's sum
+    // sum_{i<L} conj(pre_i) z_i is taken as its CP share in time plus its body
+    // share by Parseval, sum_k conj(S_k) Z_k / sqrt(N) over the preamble's
+    // nonzero bins (pre's body = IFFT(S)/sqrt(N): Frame.cpp:54-70), from the
+    // unrotated FFT Z that chan_char_lq needs anyway; that FFT of the
+    // e^{-i phi_pr}-rotated body is then e^{-i phi_pr} Z. The same quantities,
+    // rounded differently (~1e-16 relative); the 640 template loads are gone.
     const double slope0 = -2.0 * M_PI * cfo - phi[0] / N;
+    double phr;
     {
         double sn, cs, ws, wc;
         sincos(slope0 * (double)t, &sn, &cs);
@@ -879,22 +892,10 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamPa
         for (int r = 0; r < RMAX; ++r) {
             if (r < LT) {
                 z[r] = cmul_exact(z[r], c);
-                acc = cadd(acc, cconj_mul(a.pre[t + T * r], z[r]));  // pr_phase_sinh sum
+                if (r < 2 && r < CT) acc = cadd(acc, cconj_mul(prc[r], z[r]));
                 c = cmul(c, w);
             }
         }
-        acc = block_sum2<T>(acc, red);
-        if (t == 0) phpr = atan2(acc.y, acc.x);
-        __syncthreads();
-    }
-    PPROF(pc1 = clock64(); if (t == 0) atomicAdd(&g_params_prof[2], pc1 - pc0); pc0 = pc1;)
-    const double phr = phpr;
-
-    // chan_char_lq: FFT_FORM::read of the corrected preamble symbol
-    {
-        double sn, cs;
-        sincos(-phr, &sn, &cs);
-        const double2 rot = make_double2(cs, sn);
         // body sample cp + t + T*i is register CT + i: regrouped through LDS
         // (CT is a runtime count; a register select chain would cost more)
 #pragma unroll
@@ -903,13 +904,30 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) stream_params_kernel(StreamPa
         lds_barrier();
         double2 v[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = cmul_exact(fftb[t + T * i], rot);
+        for (int i = 0; i < 8; ++i) v[i] = fftb[t + T * i];
         lds_barrier();
-        fft_block<LOGN, -1>(v, t, lds_tw, fftb);
-        if (t < a.P) pil[t] = fftb[lds_swz(pbin)];  // P <= T (host-checked)
+        fft_block<LOGN, -1>(v, t, lds_tw, fftb);  // Z (unrotated)
+        const double2 pz = t < a.P ? fftb[lds_swz(pbin)] : make_double2(0.0, 0.0);  // P <= T (host-checked)
+        double2 dz[4];
+        double2 bacc = make_double2(a.pilot_ampl * pz.x, a.pilot_ampl * pz.y);  // S = pilot_ampl (real)
 #pragma unroll
-        for (int u = 0; u < 2; ++u)  // D/2 <= 2T (host-checked)
-            if (t + T * u < half) dat[t + T * u] = fftb[lds_swz(dbin[u])];
+        for (int u = 0; u < 4; ++u) {
+            dz[u] = t + T * u < a.D ? fftb[lds_swz(dbin[u])] : make_double2(0.0, 0.0);
+            bacc = cadd(bacc, cconj_mul(mpre[u], dz[u]));
+        }
+        const double isn = 1.0 / sqrt((double)N);
+        acc = cadd(acc, make_double2(bacc.x * isn, bacc.y * isn));
+        acc = block_sum2<T>(acc, red);
+        if (t == 0) phpr = atan2(acc.y, acc.x);
+        __syncthreads();
+        phr = phpr;
+        double rs2, rc2;
+        sincos(-phr, &rs2, &rc2);
+        const double2 rot = make_double2(rc2, rs2);
+        if (t < a.P) pil[t] = cmul_exact(pz, rot);
+#pragma unroll
+        for (int u = 0; u < 2; ++u)  // D/2 <= 2T
+            if (t + T * u < half) dat[t + T * u] = cmul_exact(dz[u], rot);
     }
     __syncthreads();
     PPROF(pc1 = clock64(); if (t == 0) atomicAdd(&g_params_prof[3], pc1 - pc0); pc0 = pc1;)
@@ -996,7 +1014,8 @@ hipError_t launch_stream_params(int logn, const StreamParamsArgs& a, hipStream_t
     if (a.nframes <= 0) return hipSuccess;
     // one preamble symbol, form length a multiple of T (register layout), <= 16 registers
     const int T = (1 << logn) / 8, L = (1 << logn) + a.cp;
-    if (a.npr != 1 || a.S + 1 > 64 || L % T != 0 || L / T > 16) return hipErrorInvalidValue;
+    if (a.npr != 1 || a.S + 1 > 64 || L % T != 0 || L / T > 16 || a.cp > 2 * T || a.D > 4 * T || a.P > T)
+        return hipErrorInvalidValue;
     switch (logn) {
         case 6: return params_launch_n<6>(a, st);
         case 7: return params_launch_n<7>(a, st);
