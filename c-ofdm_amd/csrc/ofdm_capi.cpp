@@ -157,6 +157,9 @@ struct ofdm_ctx {
     Grow h_walk, h_frames;
     hipStream_t h_frames_stream = nullptr;  // stream of the last copy out of h_frames
     bool h_frames_used = false;
+    int* d_queue = nullptr;        // walker chunk counter (zero between calls)
+    bool queue_zero = false;       // the last call's compaction resets it ...
+    hipEvent_t ev_qreset = nullptr;  // ... when this event completes
     hipEvent_t ev_walk = nullptr;  // walk records landed in h_walk
     hipEvent_t ev_wdone = nullptr;  // the walk kernel finished (caller's stream)
     hipStream_t side = nullptr;     // copies the walk records out beside the decode
@@ -307,6 +310,8 @@ int ofdm_destroy(ofdm_ctx* c)
         if (g->p) (void)hipFree(g->p);
     for (auto* g : {&c->h_walk, &c->h_frames})
         if (g->p) (void)hipHostFree(g->p);
+    if (c->d_queue) (void)hipFree(c->d_queue);
+    if (c->ev_qreset) (void)hipEventDestroy(c->ev_qreset);
     if (c->ev_walk) (void)hipEventDestroy(c->ev_walk);
     if (c->ev_wdone) (void)hipEventDestroy(c->ev_wdone);
     if (c->side) (void)hipStreamDestroy(c->side);
@@ -1169,7 +1174,7 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     const size_t rec_b = (size_t)nchunks * max_rec * sizeof(long);
     const size_t walk_b0 = rec_b + (size_t)nchunks * (sizeof(long) + sizeof(int)) + 2 * sizeof(long) + 64;
     const size_t walk_b = walk_b0 + 2 * (size_t)nchunks * sizeof(int);  // + in-core counts and first indices
-    if ((rc = grow(c, c->s_walk, walk_b + 64))) return rc;  // + the chunk queue counter (not copied out)
+    if ((rc = grow(c, c->s_walk, walk_b))) return rc;
     char* wb = static_cast<char*>(c->s_walk.p);
     long* d_rec = reinterpret_cast<long*>(wb);
     long* d_exit = reinterpret_cast<long*>(wb + rec_b);
@@ -1214,9 +1219,19 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     w.first_in = d_first_in;
     // the walkers take chunks from a queue: one resident round of workgroups
     // drains it, slower walkers taking fewer chunks
-    w.queue = reinterpret_cast<int*>(wb + walk_b);
+    // drains it, slower walkers taking fewer chunks. The counter is zeroed by
+    // the previous call's compaction (stream order), else here.
+    if (!c->d_queue) {
+        HIP_TRY(hipMalloc((void**)&c->d_queue, 64));
+        c->queue_zero = false;
+    }
+    w.queue = c->d_queue;
     w.nchunks = nchunks;
-    HIP_TRY(hipMemsetAsync(w.queue, 0, sizeof(int), st));
+    if (c->queue_zero)
+        HIP_TRY(hipStreamWaitEvent(st, c->ev_qreset, 0));  // no-op on the same stream
+    else
+        HIP_TRY(hipMemsetAsync(w.queue, 0, sizeof(int), st));
+    c->queue_zero = false;
     hipError_t e = ofdm::launch_stream_walk(c->t2_logn, w, std::min(nchunks, slots), st);
     if (e != hipSuccess) return hip_fail(e, "stream_walk launch");
 
@@ -1341,8 +1356,12 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
         ka.list = d_pbs;
         ka.list2 = pb_out;
         ka.count = d_pbs + ub;
+        ka.queue_reset = c->d_queue;  // after the walk (stream order): zero for the next call
         e = ofdm::launch_compact(ka, st);
         if (e != hipSuccess) return hip_fail(e, "stream compact launch");
+        if (!c->ev_qreset) HIP_TRY(hipEventCreateWithFlags(&c->ev_qreset, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(c->ev_qreset, st));
+        c->queue_zero = true;
     }
     if (spec && (rc = decode_fused(d_pbs, ub, d_pbs + ub))) return rc;
     HIP_TRY(hipEventSynchronize(c->ev_walk));

@@ -1661,7 +1661,10 @@ __global__ void __launch_bounds__(1024) compact_kernel(CompactArgs a)
         base += tot;
         __syncthreads();  // excl / srcb / wsum are rewritten by the next block
     }
-    if (t == 0) *a.count = base;
+    if (t == 0) {
+        *a.count = base;
+        if (a.queue_reset) *a.queue_reset = 0;
+    }
 }
 
 hipError_t launch_compact(const CompactArgs& a, hipStream_t st)

@@ -152,6 +152,7 @@ struct CompactArgs {
     long* list;                 // cap entries
     long* list2;                // nullable: a second copy (the caller's pb_out)
     long* count;                // total located (uncapped)
+    int* queue_reset;           // nullable: the walkers' chunk counter, zeroed at the end
 };
 hipError_t launch_compact(const CompactArgs& a, hipStream_t st);
 
