@@ -1371,6 +1371,10 @@ __global__ void __launch_bounds__(WALK_THREADS, 4) stream_walk_kernel(WalkArgs a
     int* bestg = best + 1;
     int* unsure = best + 2;
     double* scr = reinterpret_cast<double*>(best + 4);  // 16 scan / max scratch
+    // T2 first-hit block, two slots used alternately (one barrier per scan
+    // step), in scr[4] (the preamble search uses scr[0..3], [8..15]): the
+    // walker's LDS stays at 4 walkers per CU
+    int* bslot = reinterpret_cast<int*>(scr + 4);
     double2* tw_m = reinterpret_cast<double2*>(scr + 16);  // TwLds<WALK_FFT_LOGM> (FFT search)
     double2* big = tw_m + TwLds<WALK_FFT_LOGM>::SIZE;
     double2* fftb = big;                                // G * N (T2 transforms)
@@ -1384,7 +1388,12 @@ __global__ void __launch_bounds__(WALK_THREADS, 4) stream_walk_kernel(WalkArgs a
     load_twiddles<LOGT>(a.t2tw, lds_tw, t0, WALK_THREADS);
     if (a.tspec) load_twiddles<WALK_FFT_LOGM>(a.tw_m, tw_m, t0, WALK_THREADS);
     for (int i = t0; i < a.L; i += WALK_THREADS) ctap[i] = a.templ[i];
-    if (t0 == 0) *bestg = INT_MAX;
+    if (t0 == 0) {
+        *bestg = INT_MAX;
+        bslot[0] = INT_MAX;
+        bslot[1] = INT_MAX;
+    }
+    unsigned scan_it = 0;  // T2 scan steps so far (uniform): picks the bslot
     WPROF(unsigned long long p_t2 = 0, p_n2 = 0, p_pre = 0, p_np = 0, p_steps = 0;
           const unsigned long long p_w0 = wall_clock64(); const unsigned long long p_c0 = clock64();)
     // chunks: from the queue until it is drained (walkers that run slower on
@@ -1479,14 +1488,19 @@ __global__ void __launch_bounds__(WALK_THREADS, 4) stream_walk_kernel(WalkArgs a
                     sine += red[g * NW + w].y;
                 }
             }
+            // slot scan_it & 1 collects this step's first hit. The other slot
+            // was read in the previous step, before this step's barrier, and
+            // is reset here for the next step, whose atomics come after the
+            // barriers inside its transform.
+            int* hslot = bslot + (scan_it & 1);
             if (tt == 0 && live && tot != 0.0) {
                 const double rel = sine / tot;
-                if (!isnan(rel) && rel > a.t2_level) atomicMin(bestg, g);
+                if (!isnan(rel) && rel > a.t2_level) atomicMin(hslot, g);
             }
             __syncthreads();
-            const int bg = *bestg;
-            __syncthreads();  // all have read bestg
-            if (t == 0) *bestg = INT_MAX;
+            const int bg = *hslot;
+            if (t == 0) bslot[(scan_it + 1) & 1] = INT_MAX;
+            ++scan_it;
             WPROF(if (t == 0 && blockIdx.x < 8192) {
                 unsigned long long* q = g_walk_sub + 8 * blockIdx.x;
                 q[4] += r1 - r0; q[5] += clock64() - r1;
