@@ -26,6 +26,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "c-ofdm_amd", "python"))
+from ofdm_synth import payload_bytes  # noqa: E402  (counter-based job payload)
 
 METRIC = "IQ-samples/sec (tx IFFT+CP and rx FFT+equalise), 2048-subcarrier frames, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
@@ -33,6 +34,9 @@ CONFIG_B = dict(fft_size=2048, num_data_subc=1024, num_pilot_subc=32, cp_size=51
                 num_pr_symb=1, pr_sin_len=128, pr_seed=42, pr_level=500, t2sin_size=256, t2_sin_f1=17,
                 t2_sin_f2=51, t2_sin_level=800, smooth=5, mod_type=2, pilot_ampl=2500, mult=200,
                 rx_buf_size=40, iterations=10000)
+# config/config.txt (the D config of SURVEY §8): the config-4 stream's frames
+CONFIG_D = dict(CONFIG_B, fft_size=512, num_data_subc=256, num_pilot_subc=8, cp_size=128, mod_type=4)
+STREAM_WORKLOAD = "config4_stream_D_frames_gaps0-4096_cfo0.004_awgn20dB"
 
 
 def rx_bytes_per_symbol(p) -> int:
@@ -62,17 +66,6 @@ def load_pmc(workload: str):
     return best
 
 
-def payload_bytes(begin: int, count: int, seed: int = 0x5EED) -> np.ndarray:
-    """Counter-based synthetic payload: byte i of the whole job = splitmix64(seed + i) & 0xFF,
-    so every rank generates exactly its shard and the job is independent of the GPU count."""
-    z = np.arange(begin, begin + count, dtype=np.uint64) + np.uint64(seed)
-    z = z * np.uint64(0x9E3779B97F4A7C15)
-    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
-    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
-    z = z ^ (z >> np.uint64(31))
-    return (z & np.uint64(0xFF)).astype(np.uint8)
-
-
 def _cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -82,6 +75,26 @@ def _cpu_model() -> str:
     except OSError:
         pass
     return "unknown CPU"
+
+
+def granted_cpus() -> dict:
+    """CPUs this process may use: the affinity mask, capped by a cgroup v2
+    CPU quota and by OMP_NUM_THREADS, which the GPU lease sets to its CPU
+    share (a lease sees every core of the host and is granted a share)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    omp = int(omp) if omp.isdigit() and int(omp) > 0 else None  # the lease's stated CPU share
+    granted = min(v for v in (aff, quota, omp) if v)
+    return {"cpu_count": os.cpu_count(), "affinity": aff, "cgroup_quota": quota, "omp_num_threads": omp,
+            "granted": granted}
 
 
 def cpu_baseline(p, data_host: np.ndarray, noise_std: float, budget_s: float, threads: int):
@@ -119,9 +132,146 @@ def cpu_baseline(p, data_host: np.ndarray, noise_std: float, budget_s: float, th
                        f"OpenMP threads in {mt_s:.1f} s; {st_frames} frames single-threaded in {st_s:.1f} s")}
 
 
+def load_pmc_stream(workload: str):
+    """HBM traffic per stream call from a committed PMC summary
+    (profiles/pmc_stream_*.json), or None."""
+    import glob
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_stream_*.json"))):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") == workload:
+            best = d
+    return best
+
+
+def cpu_stream_baseline(p, x_host: np.ndarray, budget_s: float):
+    """The oracle's rx.cpp walk + main.cpp:60-80 decode, single-threaded as the
+    reference's rx runs, over a prefix of the same stream sized to ~budget_s."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    g = O.geometry(p)
+    span = g["preamble_len"] + g["message_len"]
+    n = 1 << 18
+    while True:
+        h = x_host[:n]
+        t0 = time.perf_counter()
+        pbs = O.stream_walk(p, h)
+        for pb in pbs:
+            if pb + span <= len(h):
+                O.decode_frame(p, h[pb:pb + span])
+        dt = time.perf_counter() - t0
+        if dt > budget_s / 3 or n >= len(x_host):
+            break
+        n = min(len(x_host), n * 4)
+    return {"value": n / dt, "unit": "stream samples/s", "cores": 1, "kind": "port",
+            "sample": f"oracle orc_stream_walk + orc_decode_frame (own FFT; FFTW absent) over the first {n} "
+                      f"samples ({len(pbs)} frames) of the same stream in {dt:.1f} s, 1 thread "
+                      f"(rx.cpp's loop is single-threaded) on {_cpu_model()}"}
+
+
+def stream_leg(args, dist, dev, world, rank, M, i16: bool):
+    """SURVEY §8d config 4 (BASELINE configs[3]): the streaming receiver (T2
+    detection walk + preamble sync + CFO/CP/phase/channel sync + demod,
+    ofdm_rx_stream_shard) over a synthetic continuous stream of D-config
+    frames. Weak scaling: the job's stream holds stream_frames frames per GPU;
+    each rank holds its core plus halo/tail (ofdm_stream.shard_stream), walks
+    and decodes it, and the ranks exchange their walk reports (ofdm_stream:
+    one small all-gather; a rank whose walk-in did not meet the true walk
+    walks again from its predecessor's exit state). One call = the whole
+    stream; value = stream samples / s."""
+    import torch
+    import ofdm_dist
+    import ofdm_stream as SS
+    import ofdm_synth as Y
+    p = dict(CONFIG_D)
+    modem = M.Modem(p, dev.index)
+    layout = Y.StreamLayout(p, args.stream_frames * world)
+    rx = SS.ShardedStreamRx(p, layout.n, world, rank)
+    nsl = rx.slice_hi - rx.slice_lo
+    x = Y.stream_slice(modem, layout, rx.slice_lo, rx.slice_hi, dev, i16=i16)
+    f0, f1 = layout.frames_overlapping(rx.slice_lo, rx.slice_hi)
+    cap = f1 - f0 + 16
+    npts = p["num_data_subc"] * p["num_symb"]
+    outs = {"pb_out": torch.full((cap,), -1, dtype=torch.int64, device=dev),
+            "bytes_out": torch.zeros((cap * layout.bpf,), dtype=torch.uint8, device=dev),
+            "constell_out": torch.zeros((cap * npts,), dtype=torch.complex128, device=dev),
+            "cfo_out": torch.zeros((cap,), dtype=torch.float64, device=dev)}
+    stream = torch.cuda.current_stream(dev)
+    walk = SS.hip_walker(modem, x, nsl, rx.own_lo - rx.slice_lo, rx.own_hi - rx.slice_lo, cap, outs, i16=i16,
+                         stream=stream)
+    exchange = SS.torch_exchange(dist, ofdm_dist.collective_device(dist, dev))
+    for _ in range(args.stream_warmup):
+        rx.run(walk, exchange)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    rx.rewalks = 0
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.stream_reps):
+        n_owned = rx.run(walk, exchange)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    elapsed = ofdm_dist.max_over_ranks(time.perf_counter() - t0, dev, dist)
+    call_ms = ev0.elapsed_time(ev1) / args.stream_reps  # this rank, its stream
+    # located frames decode to the payload of the frame placed there
+    k = min(n_owned, cap)
+    pbs = outs["pb_out"][:k].cpu().numpy() + rx.slice_lo
+    where = np.searchsorted(layout.starts, pbs, side="right") - 1
+    ok = 0
+    if k:
+        got = outs["bytes_out"][:k * layout.bpf].view(k, layout.bpf).cpu().numpy()
+        fa, fb = int(where.min()), int(where.max()) + 1
+        sent = payload_bytes(fa * layout.bpf, (fb - fa) * layout.bpf).reshape(fb - fa, layout.bpf)
+        ok = int((got == sent[where - fa]).all(axis=1).sum())
+    cdev = ofdm_dist.collective_device(dist, dev)
+    tot = torch.tensor([n_owned, ok, rx.rewalks], dtype=torch.int64, device=cdev)
+    ofdm_dist.reduce_counters(tot, dist)
+    tot = tot.cpu().numpy()
+    esz = 4 if i16 else 16
+    core = rx.own_hi - rx.own_lo
+    alg_rank = core * esz + n_owned * (16 * npts + layout.bpf)  # SURVEY §8d: stream once + outputs
+    workload = STREAM_WORKLOAD + ("_int16" if i16 else "")
+    pmc = load_pmc_stream(workload) if world == 1 else None
+    res = {"metric": "stream samples/s (T2 walk + preamble sync + CFO/CP/phase/chan sync + demod), "
+                     "config-4 stream", "workload": workload, "value": layout.n * args.stream_reps / elapsed,
+           "unit": "stream samples/s", "dtype": "f64" + (" (int16 wire input)" if i16 else ""),
+           "n_gpus": world, "scaling": "weak", "reps": args.stream_reps, "warmup": args.stream_warmup,
+           "ms_per_call": elapsed / args.stream_reps * 1e3, "stream_samples": layout.n,
+           "stream_GB": layout.n * esz / 1e9, "frames_sent": layout.total_frames, "frames_found": int(tot[0]),
+           "frames_error_free": int(tot[1]), "rewalks_per_call": int(tot[2]) / args.stream_reps,
+           "halo": rx.halo, "tail": rx.tail,
+           "roofline": {"bound": "hbm", "kernel": "whole stream pipeline (walker + compaction + cfo + params + "
+                                                  "stream rx, host stitching overlapped)",
+                        "achieved": alg_rank / (call_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": alg_rank / (call_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                        "algorithmic_bytes_per_call": alg_rank, "avg_call_ms": call_ms,
+                        "traffic": (pmc or {}).get("hbm_bytes_per_call")},
+           "cpu_baseline": None}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not i16:
+        try:
+            res["cpu_baseline"] = cpu_stream_baseline(p, x[:1 << 27].cpu().numpy(), args.stream_cpu_budget)
+        except Exception as e:  # reported, not fatal
+            res["cpu_baseline"] = {"error": repr(e)}
+    modem.close()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU). Under torch.distributed.run WORLD_SIZE decides; otherwise "
+                         "bench.py starts the N ranks itself (torch.distributed.run, 127.0.0.1)")
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                    help="nccl = RCCL over xGMI, one GPU per rank; gloo = host collectives, ranks may share "
+                         "a GPU (rehearsal of the multi-rank path on a 1-GPU box)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10, help="untimed steps (the GPU clocks ramp over the first ~10 launches)")
     ap.add_argument("--frames", type=int, default=8192, help="frames per GPU (8 symbols each); weak scaling")
@@ -129,26 +279,31 @@ def main():
                     help="strong scaling: shard this many frames over the GPUs (config 5: 30517 = 10 GB)")
     ap.add_argument("--snr-db", type=float, default=10.0)
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline (half 1 thread, half all)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: min(16, cpu_count))")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: every CPU the lease grants)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-stream", action="store_true", help="skip the config-4 stream sub-record")
+    ap.add_argument("--stream-frames", type=int, default=16384, help="config-4 stream frames per GPU (weak)")
+    ap.add_argument("--stream-reps", type=int, default=10)
+    ap.add_argument("--stream-warmup", type=int, default=3)
+    ap.add_argument("--stream-cpu-budget", type=float, default=8.0)
     args = ap.parse_args()
 
-    import torch
     import ofdm_dist
+    if ofdm_dist.needs_launch(args.gpus):
+        # one process per GPU: the ranks are children of this process, which
+        # never touches the GPU itself; rank 0 prints the JSON line
+        sys.exit(ofdm_dist.launch_ranks(args.gpus, os.path.abspath(__file__), sys.argv[1:]))
+
+    import torch
     import ofdm_mi355x as M
 
     world, rank, local = ofdm_dist.env_world()
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: WORLD_SIZE={world} (launcher) overrides --gpus {args.gpus}", file=sys.stderr)
+    dist, dev = ofdm_dist.init(args.backend, local)
 
     p = dict(CONFIG_B)
-    modem = M.Modem(p, local)
+    modem = M.Modem(p, dev.index)
     geo = modem.geo
     strong = args.total_frames > 0
     if strong:
@@ -239,6 +394,7 @@ def main():
             "mod_type": p["mod_type"], "frames_per_gpu": nf, "symbols_per_gpu": nf * S,
             "total_frames": args.total_frames if strong else world * nf,
             "samples_per_step_per_gpu": nf * msg, "parallelism": f"frame-sharded x{world}",
+            "backend": args.backend if world > 1 else None,
         },
         "roofline": {
             "bound": "hbm",
@@ -262,13 +418,20 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            thr = args.cpu_threads or min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16
+            cpus = granted_cpus()
+            thr = args.cpu_threads or cpus["granted"]
             result["cpu_baseline"] = cpu_baseline(p, data_host, noise_std, args.cpu_budget, thr)
+            result["cpu_baseline"]["host_cpus"] = cpus
         except Exception as e:  # reported, not fatal: the GPU number stands alone
             result["cpu_baseline"] = {"error": repr(e)}
+    modem.close()
+    if not args.no_stream:
+        del iq, cons, out, data
+        torch.cuda.empty_cache()
+        result["stream"] = stream_leg(args, dist, dev, world, rank, M, i16=False)
+        result["stream_int16"] = stream_leg(args, dist, dev, world, rank, M, i16=True)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    modem.close()
     if dist:
         dist.destroy_process_group()
 

@@ -1132,13 +1132,20 @@ int ofdm_sync_frames(ofdm_ctx* c, double* frames, size_t nframes, size_t stride,
 
 }  // extern "C"
 
-// ofdm_rx_stream / ofdm_rx_stream_i16: exactly one of iq, iq16 is set.
+// ofdm_rx_stream / ofdm_rx_stream_i16 / ofdm_rx_stream_shard: exactly one of
+// iq, iq16 is set. The walk starts at state `start`; frames located with pb in
+// [own_lo, own_hi) are decoded (the whole stream: start = own_lo = 0, own_hi = n).
 static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, size_t n, size_t max_frames,
                           long chunk, long* pb_out, uint8_t* bytes_out, double* constell_out, double* cfo_out,
-                          size_t* nframes_out, void* stream)
+                          size_t* nframes_out, void* stream, long start, long own_lo, long own_hi,
+                          long* located, size_t located_cap, size_t* nlocated_out, long* exit_out)
 {
     if (!c || (!iq && !iq16) || !nframes_out) return fail(OFDM_ERR_INVALID, "null argument");
     *nframes_out = 0;
+    if (nlocated_out) *nlocated_out = 0;
+    if (exit_out) *exit_out = -1;
+    if (start < 0 || own_lo < 0 || own_lo > own_hi || own_hi > (long)n)
+        return fail(OFDM_ERR_INVALID, "need 0 <= start, 0 <= own_lo <= own_hi <= n");
     if (c->t2_logn < 6 || c->t2_logn > 11) return fail(OFDM_ERR_UNSUPPORTED, "stream walk needs T2sin_size = 2^a, 64..2048");
     if ((iq && !aligned16(iq)) || (iq16 && ((uintptr_t)iq16 & 3)) || (constell_out && !aligned16(constell_out)))
         return fail(OFDM_ERR_INVALID, "misaligned buffer (complex<double> 16 B, complex<int16> 4 B)");
@@ -1146,7 +1153,7 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     hipStream_t st = (hipStream_t)stream;
     const long L = c->L, pre = (long)L * c->npr, msg = (long)L * c->S, span = pre + msg;
     const long flen = c->geo.frame_len, nn = (long)n;
-    if (nn == 0) return OFDM_OK;
+    if (nn == 0 || start >= nn) return OFDM_OK;
     // walkers: one chunk per resident walker slot (a single round: every
     // chunk re-walks a 3-frame halo to meet the true walk, so fewer, longer
     // chunks cost less), each >= 8 frames
@@ -1159,17 +1166,20 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     const char* eq = getenv("OFDM_WALK_Q");
     const char* eh = getenv("OFDM_WALK_HALO");
     const long qper = eq ? std::max(1L, atol(eq)) : 1;
-    if (chunk <= 0) chunk = std::max(8 * flen, (nn + slots * qper - 1) / (slots * qper));
+    const long span_w = own_hi - own_lo;  // the chunk cores tile [own_lo, own_hi)
+    if (chunk <= 0) chunk = std::max(8 * flen, (span_w + slots * qper - 1) / (slots * qper));
     chunk = std::max(chunk, (long)c->t2);
     const long halo = eh ? std::max(0L, atol(eh)) * flen / 1000 : 3 * flen;
     const char* ee = getenv("OFDM_WALK_EXT");
     const long ext = ee ? std::max(0L, atol(ee)) * flen / 1000 : 0;
-    const long nchunks = (nn + chunk - 1) / chunk;
+    const long nchunks = std::max(1L, (span_w + chunk - 1) / chunk);
     if (nchunks > 1 << 20) return fail(OFDM_ERR_INVALID, "chunk too small for this stream");
     // each located frame advances the walk by > message_len, and a walker can
     // walk on past its core end by ext plus one scan step (256 threads x 8
     // samples) and the preamble window: this many records always suffice
-    const int max_rec = (int)((chunk + halo + ext + 2048 + 2 * c->p.t2sin_size + c->p.pr_sin_len) / msg + 4);
+    // (chunk 0 walks in from `start`, the others a halo before their core)
+    const int max_rec =
+        (int)((chunk + std::max(halo, own_lo - start) + ext + 2048 + 2 * c->p.t2sin_size + c->p.pr_sin_len) / msg + 4);
     int rc;
     const size_t rec_b = (size_t)nchunks * max_rec * sizeof(long);
     const size_t walk_b0 = rec_b + (size_t)nchunks * (sizeof(long) + sizeof(int)) + 2 * sizeof(long) + 64;
@@ -1210,6 +1220,9 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     w.msg = msg;
     w.chunk = chunk;
     w.halo = halo;
+    w.start = start;
+    w.core_lo = own_lo;
+    w.core_hi = own_hi;
     w.ext = ext;
     w.max_rec = max_rec;
     w.rec = d_rec;
@@ -1370,7 +1383,7 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     std::vector<long> spec_list;
     if (spec)
         for (long k = 0; k < nchunks; ++k) {
-            const long lo = k * chunk, hi = lo + chunk;
+            const long lo = own_lo + k * chunk, hi = std::min(lo + chunk, own_hi);
             for (int i = 0; i < std::min(nrec[k], max_rec); ++i) {
                 const long pb = rec[(size_t)k * max_rec + i];
                 if (pb >= lo && pb < hi) spec_list.push_back(pb);
@@ -1401,14 +1414,14 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
         HIP_TRY(hipStreamSynchronize(st));
         return OFDM_OK;
     };
-    std::vector<long> frames;
+    std::vector<long> frames, walk_in;
     std::vector<long> prev;  // every frame the accepted walk of the previous chunk located
-    long texit = 0;
+    long texit = 0, last_k = -1;
     for (long k = 0; k < nchunks; ++k) {
         if (k > 0 && texit < 0) break;  // the true walk ended
         if (nrec[k] > max_rec) return fail(OFDM_ERR_HIP, "stream walk record overflow");
         std::vector<long> lst(rec + (size_t)k * max_rec, rec + (size_t)k * max_rec + nrec[k]);
-        const long lo = k * chunk, hi = lo + chunk;
+        const long lo = own_lo + k * chunk, hi = std::min(lo + chunk, own_hi);
         if (k > 0) {
             long first_owned = LONG_MAX;
             for (long pb : lst)
@@ -1422,12 +1435,28 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
                 lst.assign(rec + (size_t)k * max_rec, rec + (size_t)k * max_rec + nrec[k]);
             }
         }
+        if (k == 0)  // the walk-in from `start` (true by definition): frames before own_lo
+            for (long pb : lst)
+                if (pb < lo) walk_in.push_back(pb);
         for (long pb : lst)
             if (pb >= lo && pb < hi) frames.push_back(pb);
         prev.swap(lst);
         texit = ex[k];
+        last_k = k;
     }
     *nframes_out = frames.size();
+    if (exit_out) *exit_out = last_k == nchunks - 1 ? texit : -1;
+    if (nlocated_out) {
+        // every frame of the stitched walk: the walk-in, the owned frames, and
+        // what the last walker located past own_hi before it stopped
+        std::vector<long> all(walk_in);
+        all.insert(all.end(), frames.begin(), frames.end());
+        if (last_k == nchunks - 1)
+            for (long pb : prev)
+                if (pb >= own_hi) all.push_back(pb);
+        *nlocated_out = all.size();
+        if (located) std::memcpy(located, all.data(), std::min(all.size(), located_cap) * sizeof(long));
+    }
     if (getenv("OFDM_STREAM_DEBUG"))
         fprintf(stderr, "ofdm_rx_stream: %ld chunks of %ld samples, halo %ld, %ld re-walks, %zu frames, speculative %s\n",
                 nchunks, chunk, halo, nrewalk, frames.size(), spec ? (frames == spec_list ? "hit" : "miss") : "off");
@@ -1483,7 +1512,7 @@ int ofdm_rx_stream(ofdm_ctx* c, const double* iq, size_t n, size_t max_frames, l
 {
     if (!iq) return fail(OFDM_ERR_INVALID, "null argument");
     return rx_stream_impl(c, iq, nullptr, n, max_frames, chunk, pb_out, bytes_out, constell_out, cfo_out,
-                          nframes_out, stream);
+                          nframes_out, stream, 0, 0, (long)n, nullptr, 0, nullptr, nullptr);
 }
 
 int ofdm_rx_stream_i16(ofdm_ctx* c, const int16_t* iq16, size_t n, size_t max_frames, long chunk, long* pb_out,
@@ -1491,7 +1520,17 @@ int ofdm_rx_stream_i16(ofdm_ctx* c, const int16_t* iq16, size_t n, size_t max_fr
 {
     if (!iq16) return fail(OFDM_ERR_INVALID, "null argument");
     return rx_stream_impl(c, nullptr, iq16, n, max_frames, chunk, pb_out, bytes_out, constell_out, cfo_out,
-                          nframes_out, stream);
+                          nframes_out, stream, 0, 0, (long)n, nullptr, 0, nullptr, nullptr);
+}
+
+int ofdm_rx_stream_shard(ofdm_ctx* c, const double* iq, const int16_t* iq16, size_t n, long start, long own_lo,
+                         long own_hi, size_t max_frames, long chunk, long* pb_out, uint8_t* bytes_out,
+                         double* constell_out, double* cfo_out, size_t* nframes_out, long* located,
+                         size_t located_cap, size_t* nlocated_out, long* exit_out, void* stream)
+{
+    if (!iq == !iq16) return fail(OFDM_ERR_INVALID, "exactly one of iq, iq16");
+    return rx_stream_impl(c, iq, iq16, n, max_frames, chunk, pb_out, bytes_out, constell_out, cfo_out,
+                          nframes_out, stream, start, own_lo, own_hi, located, located_cap, nlocated_out, exit_out);
 }
 
 }  // extern "C"

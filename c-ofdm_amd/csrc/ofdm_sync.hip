@@ -1410,8 +1410,10 @@ __global__ void __launch_bounds__(WALK_THREADS, 4) stream_walk_kernel(WalkArgs a
         if (round > 0) break;
         c = a.chunk_ids ? a.chunk_ids[blockIdx.x] : (int)blockIdx.x;
     }
-    const long core0 = (long)c * a.chunk, end = core0 + a.chunk;
-    long pos = a.start_pos ? a.start_pos[blockIdx.x] : (c == 0 ? 0 : (core0 > a.halo ? core0 - a.halo : 0));
+    // chunk cores tile [core_lo, core_hi); chunk 0 walks in from the given
+    // start state, the others from a halo before their core
+    const long core0 = a.core_lo + (long)c * a.chunk, end = min(core0 + a.chunk, a.core_hi);
+    long pos = a.start_pos ? a.start_pos[blockIdx.x] : (c == 0 ? a.start : (core0 > a.halo ? core0 - a.halo : 0));
     int nrec = 0, ncore = 0, first_in = 0;
     long exitp = -1;
     bool past = false;  // a frame at or past the core end is located

@@ -86,6 +86,8 @@ struct WalkArgs {
     double pr_level;
     long pre, msg;              // preamble / message lengths (samples)
     long chunk, halo;           // core samples per chunk; walk-in before the core
+    long start;                 // walk state chunk 0 starts from (0: the stream's first sample)
+    long core_lo, core_hi;      // the chunk cores tile [core_lo, core_hi) (whole stream: [0, n))
     long ext;                   // walk-on past the core end while looking for the first frame there
     const int* chunk_ids;       // nullable: chunk of each workgroup (re-walk launches)
     const long* start_pos;      // nullable: exact start state per workgroup (re-walk)

@@ -102,6 +102,8 @@ SIGNATURES = {
     "ofdm_sync_frames": (_I, [_V, _V, _SZ, _SZ, _I, _V, _V, _V, _V]),
     "ofdm_rx_stream": (_I, [_V, _V, _SZ, _SZ, _L, _V, _V, _V, _V, C.POINTER(_SZ), _V]),
     "ofdm_rx_stream_i16": (_I, [_V, _V, _SZ, _SZ, _L, _V, _V, _V, _V, C.POINTER(_SZ), _V]),
+    "ofdm_rx_stream_shard": (_I, [_V, _V, _V, _SZ, _L, _L, _L, _SZ, _L, _V, _V, _V, _V, C.POINTER(_SZ), _V, _SZ,
+                                  C.POINTER(_SZ), C.POINTER(_L), _V]),
 }
 
 _lib = None
@@ -308,6 +310,25 @@ class Modem:
         check(lib().ofdm_rx_stream_i16(self.h, _ptr(iq16), n, max_frames, chunk, _ptr(pb_out), _ptr(bytes_out),
                                        _ptr(constell_out), _ptr(cfo_out), C.byref(m), _stream(stream)))
         return m.value
+
+    def rx_stream_shard(self, iq, n: int, start: int, own_lo: int, own_hi: int, max_frames: int, pb_out=None,
+                        bytes_out=None, constell_out=None, cfo_out=None, chunk: int = 0, i16: bool = False,
+                        located_cap: int = 4096, stream=None):
+        """ofdm_rx_stream_shard: the walk from state `start` over this shard's n
+        samples, frames with pb in [own_lo, own_hi) decoded. Returns (frames
+        decoded, located pbs (numpy int64, relative), exit state)."""
+        import numpy as np
+        m, nl, ex = C.c_size_t(), C.c_size_t(), C.c_long()
+        loc = self._located if getattr(self, "_located", None) is not None and \
+            len(self._located) >= max(1, located_cap) else np.empty(max(1, located_cap), dtype=np.int64)
+        self._located = loc
+        check(lib().ofdm_rx_stream_shard(self.h, None if i16 else _ptr(iq), _ptr(iq) if i16 else None, n, start,
+                                         own_lo, own_hi, max_frames, chunk, _ptr(pb_out), _ptr(bytes_out),
+                                         _ptr(constell_out), _ptr(cfo_out), C.byref(m), loc.ctypes.data,
+                                         located_cap, C.byref(nl), C.byref(ex), _stream(stream)))
+        if nl.value > located_cap:
+            raise OfdmError(-1, f"located list of {nl.value} frames exceeds located_cap={located_cap}")
+        return m.value, loc[:nl.value].copy(), ex.value
 
     def sync_frames(self, frames, nframes: int, frame_stride: int, stages: int = SYNC_ALL,
                     cfo_in=None, cfo_out=None, chan_out=None, stream=None):

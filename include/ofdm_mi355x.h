@@ -302,6 +302,31 @@ int ofdm_rx_stream_i16(ofdm_ctx* ctx, const int16_t* iq16, size_t n, size_t max_
                        long* pb_out, uint8_t* bytes_out, double* constell_out, double* cfo_out,
                        size_t* nframes_out, void* stream);
 
+/* One shard of a longer stream (multi-GPU streaming rx; the
+ * reference's rx.cpp:145-156 carries one frame from ring to ring, this is the
+ * same hand-over between GPUs). Exactly one of iq (complex f64) / iq16
+ * (complex<int16>) is set; it holds the shard's n samples: its core plus a
+ * walk-in halo before it and a tail after it. The walk starts at state
+ * `start` (0 = the first sample of the whole stream, or the predecessor
+ * shard's exit state; any other position gives a speculative walk that the
+ * caller checks, see c-ofdm_amd/python/ofdm_stream.py) and the frames located
+ * with pb in [own_lo, own_hi) are decoded into the outputs exactly as
+ * ofdm_rx_stream does (pb_out relative to iq). Requires 0 <= start and
+ * 0 <= own_lo <= own_hi <= n (a start past own_lo owns only frames after it:
+ * the walk moves forward).
+ *   *exit_out: the walk's first state at or past own_hi (where the next
+ *     shard's walk resumes; a position equivalent to it, or the state whose
+ *     step located the first frame past own_hi), -1 if the samples ran out.
+ *   located (host, nullable, located_cap entries) / *nlocated_out (nullable):
+ *     every frame the walk located from `start` until it stopped: those before
+ *     own_lo, the owned ones, and any located past own_hi.
+ * ofdm_rx_stream(iq, n) is ofdm_rx_stream_shard(iq, n, 0, 0, n). */
+int ofdm_rx_stream_shard(ofdm_ctx* ctx, const double* iq, const int16_t* iq16, size_t n,
+                         long start, long own_lo, long own_hi, size_t max_frames, long chunk,
+                         long* pb_out, uint8_t* bytes_out, double* constell_out, double* cfo_out,
+                         size_t* nframes_out, long* located, size_t located_cap,
+                         size_t* nlocated_out, long* exit_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

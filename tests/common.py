@@ -64,3 +64,19 @@ def rel_err(a, b) -> float:
     if a.size == 0:
         return 0.0
     return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-300))
+
+
+def impaired_stream(cfg, nf, seed, snr_db=20.0, cfo_max=0.004, gap_max=4096):
+    """Config-4 stream: full frames (T2+preamble+message) with random 0..gap_max
+    zero gaps, per-frame CFO U(-cfo_max, cfo_max) and phase, AWGN over all."""
+    g = O.geometry(cfg)
+    rng = np.random.default_rng(seed)
+    data = payload(nf * g["bytes_per_frame"], seed)
+    parts = [np.zeros(int(rng.integers(0, gap_max + 1)), np.complex128)]
+    for f in range(nf):
+        fr = O.frame_write(cfg, data[f * g["bytes_per_frame"]:(f + 1) * g["bytes_per_frame"]])
+        n = np.arange(len(fr))
+        fr = fr * np.exp(2j * np.pi * rng.uniform(-cfo_max, cfo_max) * n + 1j * rng.uniform(-np.pi, np.pi))
+        parts += [fr, np.zeros(int(rng.integers(0, gap_max + 1)), np.complex128)]
+    x = np.concatenate(parts)
+    return O.awgn(x, 10 ** (-snr_db / 20), seed=seed), data

@@ -1,0 +1,45 @@
+"""bench.py's multi-rank path on the GPU: `--gpus 2 --backend gloo` starts two
+ranks itself (ofdm_dist.launch_ranks) that share the box's one MI355X, each
+running the HIP modem on its frame shard; the job's reduced counters equal a
+single-rank run over the same global frames (the payload and the AWGN are
+counter-based functions of the global byte / sample index). RCCL itself needs
+one GPU per rank, so the nccl backend runs only on the driver's 8-GPU node."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _bench(*argv, timeout=240):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *argv], env=env, capture_output=True,
+                       text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_two_ranks_equal_one_rank_over_the_same_frames():
+    common = ["--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-stream"]
+    one = _bench("--frames", "128", *common)
+    two = _bench("--gpus", "2", "--backend", "gloo", "--frames", "64", *common)
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+    assert two["config"]["total_frames"] == 128 and two["config"]["backend"] == "gloo"
+    assert two["frames"] == one["frames"] == 2 * 128
+    assert two["bit_errors"] == one["bit_errors"] > 0
+    assert two["value"] > 0 and two["roofline"]["frac"] > 0
+
+
+def test_bench_strong_scaling_shards_total_frames():
+    common = ["--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-stream"]
+    one = _bench("--total-frames", "101", *common)
+    three = _bench("--gpus", "3", "--backend", "gloo", "--total-frames", "101", *common)
+    assert three["scaling"] == "strong" and three["n_gpus"] == 3
+    assert three["frames"] == one["frames"] == 101
+    assert three["bit_errors"] == one["bit_errors"]

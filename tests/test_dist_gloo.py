@@ -80,3 +80,47 @@ def test_two_rank_shard_and_reduce_equals_single_rank():
     assert counters == [errs, NF * g["bytes_per_frame"] * 8, NF * g["message_len"], NF]
     joined = np.concatenate([o for _, o in sorted(parts, key=lambda t: t[0])])
     assert np.array_equal(joined, out)
+
+
+def test_launcher_starts_ranks_and_reduction_equals_single_rank():
+    """ofdm_dist.launch_ranks (bench.py --gpus N) spawns 2 ranks under
+    torch.distributed.run; each sees WORLD_SIZE=2, the shards tile the batch,
+    the reduced counters and the joined bytes equal the single-rank run, and
+    rank 0 reports n_gpus=2 and the max over ranks of the elapsed time."""
+    import json
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dist_job_cpu.py")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    os.environ.pop("WORLD_SIZE", None)
+    assert ofdm_dist.needs_launch(2) and not ofdm_dist.needs_launch(1)
+    rc, out = ofdm_dist.launch_ranks(2, script, ["--frames", str(NF)], env=env, capture=True)
+    assert rc == 0, out
+    line = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(line) == 1, out  # rank 0 only
+    res = json.loads(line[0])
+    assert res["n_gpus"] == 2
+    assert [w for _, w, _, _ in res["ranks"]] == [2, 2]
+    assert [(b, c) for _, _, b, c in res["ranks"]] == [ofdm_dist.shard(NF, 2, r) for r in range(2)]
+    assert res["max_elapsed"] == 2.0
+    g = O.geometry(D)
+    data = np.random.default_rng(5).integers(0, 256, NF * g["bytes_per_frame"], dtype=np.uint8)
+    iq = O.awgn(O.tx_batch(D, data, NF), 0.45, seed=7)
+    _, out1, errs = O.rx_batch(D, iq, NF, g["message_len"], ref=data)
+    assert res["totals"] == [errs, NF * g["bytes_per_frame"] * 8, NF * g["message_len"], NF]
+    assert bytes.fromhex(res["bytes_hex"]) == out1.tobytes()
+
+
+def test_bench_gpus_flag_launches_ranks(monkeypatch):
+    """bench.py --gpus 4 without a launcher environment hands off to
+    ofdm_dist.launch_ranks with its own path and argv (before any GPU call)."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    calls = []
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(ofdm_dist, "launch_ranks", lambda n, script, argv: calls.append((n, script, argv)) or 0)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "3"])
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 0
+    assert calls == [(4, os.path.join(root, "bench.py"), ["--gpus", "4", "--steps", "3"])]

@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from common import B, D, G, golden, payload, rel_err
+from common import B, D, G, golden, impaired_stream, payload, rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -34,22 +34,6 @@ def host(t):
 
 
 GD = golden()
-
-
-def impaired_stream(cfg, nf, seed, snr_db=20.0, cfo_max=0.004, gap_max=4096):
-    """Config-4 stream: full frames (T2+preamble+message) with random 0..gap_max
-    zero gaps, per-frame CFO U(-cfo_max, cfo_max) and phase, AWGN over all."""
-    g = O.geometry(cfg)
-    rng = np.random.default_rng(seed)
-    data = payload(nf * g["bytes_per_frame"], seed)
-    parts = [np.zeros(int(rng.integers(0, gap_max + 1)), np.complex128)]
-    for f in range(nf):
-        fr = O.frame_write(cfg, data[f * g["bytes_per_frame"]:(f + 1) * g["bytes_per_frame"]])
-        n = np.arange(len(fr))
-        fr = fr * np.exp(2j * np.pi * rng.uniform(-cfo_max, cfo_max) * n + 1j * rng.uniform(-np.pi, np.pi))
-        parts += [fr, np.zeros(int(rng.integers(0, gap_max + 1)), np.complex128)]
-    x = np.concatenate(parts)
-    return O.awgn(x, 10 ** (-snr_db / 20), seed=seed), data
 
 
 def run_stream(cfg, x, max_frames=4096, chunk=0):
