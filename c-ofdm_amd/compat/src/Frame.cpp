@@ -4,6 +4,7 @@
 // the result back with the reference's in-place semantics.
 #include "OFDM/Frame.hpp"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 
@@ -153,14 +154,30 @@ std::vector<double> T2SIN_FORM::corr(complex_vector& signal)
 int T2SIN_FORM::find_t2sin(complex_vector& signal, int start_index)
 {
     COMPAT_TRACE("T2SIN_FORM::find_t2sin");
-    const size_t n = signal.size();
-    void* dx = ctx_->buf(0, n * CD);
+    // Frame.hpp:150-197 tests the blocks start + b*size in order and returns
+    // the first above the level; each block's decision reads only its own
+    // samples. So the ring goes up in windows of whole blocks from
+    // start_index (a frame or two first, then doubling) and the scan stops
+    // at the first window with a hit: rx.cpp's per-frame call moves a few
+    // frames' samples over PCIe instead of the whole ring.
+    const long n = (long)signal.size();
+    if (size <= 0 || start_index < 0 || start_index > n) return -1;
+    const long nblocks = (n - start_index) / size;
     int* df = (int*)ctx_->buf(2, sizeof(int));
-    ctx_->h2d(dx, signal.data(), n * CD);
-    check(ofdm_t2_scan(ctx_->ctx, (const double*)dx, n, start_index, nullptr, df, nullptr), "ofdm_t2_scan");
-    int first = -1;
-    ctx_->d2h(&first, df, sizeof(int));
-    return first;
+    long b0 = 0, w = std::max<long>(16, 2L * ctx_->geo.frame_len / size + 2);
+    while (b0 < nblocks) {
+        const long nb = std::min(w, nblocks - b0);
+        const size_t len = (size_t)nb * size;
+        void* dx = ctx_->buf(0, len * CD);
+        ctx_->h2d(dx, signal.data() + start_index + b0 * size, len * CD);
+        check(ofdm_t2_scan(ctx_->ctx, (const double*)dx, len, 0, nullptr, df, nullptr), "ofdm_t2_scan");
+        int first = -1;
+        ctx_->d2h(&first, df, sizeof(int));
+        if (first >= 0) return (int)(start_index + b0 * size + first);
+        b0 += nb;
+        w *= 2;
+    }
+    return -1;
 }
 
 // ---------------------------------------------------------------- OFDM_FORM
@@ -326,21 +343,45 @@ void PREAMBLE_FORM::find_corr(complex_vector& input, int start)
 int PREAMBLE_FORM::find_preamble(complex_vector& input, int start)
 {
     COMPAT_TRACE("PREAMBLE_FORM::find_preamble");
-    const size_t n = input.size();
-    void* dx = ctx_->buf(5, n * CD);
+    // Frame.cpp:338-378 reads input[start .. start + cor.size() + pr_sin_len):
+    // only that window goes to the device (samples past the vector's end
+    // read as zero in the kernel, as before)
+    const long n = (long)input.size();
+    if (start < 0 || start >= n) return -10;
+    const long win = std::min<long>(n - start, (long)cor.size() + pr_sin_len);
+    void* dx = ctx_->buf(5, (size_t)win * CD);
     int* ds = (int*)ctx_->buf(7, 2 * sizeof(int));
-    ctx_->h2d(dx, input.data(), n * CD);
-    ctx_->h2d(ds, &start, sizeof(int));
-    check(ofdm_find_preamble(ctx_->ctx, (const double*)dx, n, ds, 1, ds + 1, nullptr), "ofdm_find_preamble");
+    const int zero = 0;
+    ctx_->h2d(dx, input.data() + start, (size_t)win * CD);
+    ctx_->h2d(ds, &zero, sizeof(int));
+    check(ofdm_find_preamble(ctx_->ctx, (const double*)dx, (size_t)win, ds, 1, ds + 1, nullptr), "ofdm_find_preamble");
     int idx = -10;
     ctx_->d2h(&idx, ds + 1, sizeof(int));
-    return idx;
+    return idx < 0 ? idx : idx + start;
 }
 
 complex_vector PREAMBLE_FORM::chan_char()
 {
     COMPAT_TRACE("PREAMBLE_FORM::chan_char");
-    // the unused averaging estimator (Frame.hpp:375-385) on the GPU FFT output
+    // the averaging estimator (Frame.hpp:375-385), unused by the apps. One
+    // preamble symbol (the reference's config): pr / mod_preamble is
+    // FFT_FORM::read with mod_preamble as the caller-side divisor, which
+    // ofdm_rx_demod applies (same complex division), and the average over one
+    // symbol divides by (1, 0), an identity: all on the GPU.
+    if (num_symb == 1) {
+        void* dx = ctx_->buf(1, (size_t)size * CD);
+        void* dm = ctx_->buf(3, (size_t)num_data_subc * CD);
+        void* dc = ctx_->buf(2, (size_t)num_data_subc * CD);
+        ctx_->h2d(dx, output[0], (size_t)size * CD);
+        ctx_->h2d(dm, mod_preamble.data(), (size_t)num_data_subc * CD);
+        check(ofdm_rx_demod(ctx_->ctx, (const double*)dx, 1, (size_t)size, (const double*)dm, 0, (double*)dc, nullptr,
+                            nullptr, nullptr, nullptr),
+              "ofdm_rx_demod");
+        ctx_->d2h(chan_est.data(), dc, (size_t)num_data_subc * CD);
+        return chan_est;
+    }
+    // several preamble symbols: FFT_FORM::read on the GPU (fft()), then the
+    // caller-side per-carrier division and average, as the reference's caller code
     complex_vector pr = fft();
     std::fill(chan_est.begin(), chan_est.end(), complex_double(0.0, 0.0));
     for (int i = 0; i < num_data_subc * num_symb; i++) chan_est[i % num_data_subc] += pr[i] / mod_preamble[i];

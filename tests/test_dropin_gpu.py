@@ -131,3 +131,43 @@ def test_reference_tx_app_frames_decode(tmp_path):
     got = out.cpu().numpy().reshape(nfr, -1)[:, 8:].tobytes()
     assert got == body
     m.close()
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(REF_BIN, "main")), reason="drop-in reference apps not built")
+def test_reference_main_writes_python_code_file_contract(tmp_path):
+    """The files the reference's main.cpp:74-78 writes for python_code/ofdm.py
+    (and graph.py), from the reference's own main on the golden G config and
+    payload: data/source.bin equals the reference's committed capture bit for
+    bit; data.bin, t2_sin_corr.bin, phases.bin and constell.bin have the flat
+    f64 layouts ofdm.py:9-54 reads (x[::2] + 1j*x[1::2] for complex), and
+    their contents equal the oracle's computation on the written data.bin
+    (T2 correlation, the main.cpp:52-71 sync chain and equalised points)."""
+    write_config(tmp_path, G)
+    os.makedirs(tmp_path / "data")
+    (tmp_path / "WARANDPEACE.txt").write_bytes(GD["payload_text"].tobytes() * 4)
+    r = run([os.path.join(REF_BIN, "main")], tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "ACCURACY: 1\n" in r.stdout, r.stdout
+    g = O.geometry(G)
+    d = tmp_path / "data"
+    assert np.array_equal(np.fromfile(d / "source.bin", np.int16), GD["source"])
+    # python_code/ofdm.py's readers
+    raw = np.fromfile(d / "data.bin", dtype=np.float64)
+    x = raw[::2] + 1j * raw[1::2]
+    ring_len = g["frame_len"] * (G["rx_buf_size"] + 1)  # FRAME_FORM::from_sdr_buf (Frame.cpp:229)
+    assert x.size == ring_len
+    corr = np.fromfile(d / "t2_sin_corr.bin", dtype=np.float64)
+    assert corr.size == ring_len // G["t2sin_size"]
+    assert np.abs(corr - O.t2_corr(G, x)).max() < 1e-12
+    ph = np.fromfile(d / "phases.bin", dtype=np.float64)
+    ph = ph[::2] + 1j * ph[1::2]
+    assert ph.size == G["num_data_subc"]
+    assert np.abs(np.abs(ph) - 1).max() < 1e-12
+    cons = np.fromfile(d / "constell.bin", dtype=np.float64)
+    cons = cons[::2] + 1j * cons[1::2]
+    assert cons.size == g["npts"]
+    hit = O.find_t2sin(G, x, 0)
+    pb = O.find_preamble(G, x, hit) + 1
+    _, ocons, obytes = O.decode_frame(G, x[pb: pb + g["preamble_len"] + g["message_len"]])
+    assert np.abs(cons - ocons).max() / np.abs(ocons).max() < 1e-9
+    assert obytes.tobytes() == GD["payload"].tobytes()

@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""Per-frame time of the reference's OWN rx.cpp loop running on the drop-in
+layer (oracle/_ref/rx: rx.cpp compiled unchanged against c-ofdm_amd/compat),
+from the LOG.txt its TIME_TRACE macros write (rx.cpp:31-43,240-244), next to
+the reference's committed LOG.txt (its authors' CPU/FFTW run).
+
+The reference's tx.cpp (oracle/_ref/tx, also on the drop-in layer) frames a
+payload file into data/tx.bin-layout int16 IQ through the SDR stand-in; rx
+then reads that capture through the stand-in (OFDM_SDR_RX_FILE) with the
+radio's refill pacing. An iteration that decoded a frame (SEQ field) and did
+not refill the ring (no SDR field) is one frame's processing: find_t2sin,
+find_preamble, the sync chain, FFT, equalise, demod, MAC.
+
+  python tools/dropin_rx_timing.py [--frames 200] > profiles/<name>.json
+"""
+import argparse
+import json
+import os
+import re
+import statistics
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "c-ofdm_amd", "python")]
+REF_BIN = os.path.join(ROOT, "oracle", "_ref")
+
+
+def parse_log(text):
+    frames, refills = [], []
+    for line in text.splitlines():
+        kv = dict(re.findall(r"(\w+):(\S+)", line))
+        if "TIME" not in kv:
+            continue
+        if "SEQ" in kv and "SDR" not in kv:
+            frames.append(float(kv["TIME"]))
+        elif "SDR" in kv:
+            refills.append(float(kv.get("CONVERT", "nan")))
+    return frames, refills
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=200)
+    args = ap.parse_args()
+    from test_dropin_gpu import D, O, write_config
+    g = O.geometry(D)
+    with tempfile.TemporaryDirectory() as d:
+        write_config(d, D, iterations=args.frames + 40)
+        pay = g["bytes_per_frame"] - 8
+        body = bytes((i * 131 + 7) & 0xFF for i in range(args.frames * pay))
+        with open(os.path.join(d, "FlyMeToTheMoon_mono.wav"), "wb") as f:
+            f.write(body)
+        txf = os.path.join(d, "tx.bin")
+        env = dict(os.environ, OFDM_SDR_TX_FILE=txf)
+        r = subprocess.run([os.path.join(REF_BIN, "tx")], cwd=d, env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        env = dict(os.environ, OFDM_SDR_RX_FILE=txf)
+        r = subprocess.run([os.path.join(REF_BIN, "rx")], cwd=d, env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        with open(os.path.join(d, "LOG.txt")) as f:
+            ours, refills = parse_log(f.read())
+        with open(os.path.join(d, "Res.wav"), "rb") as f:
+            res = f.read()
+    chunks = {body[i * pay:(i + 1) * pay] for i in range(args.frames)}
+    out = {"what": "rx.cpp per-frame iteration time (LOG.txt TIME of iterations that decoded a frame without a "
+                   "ring refill), reference rx.cpp compiled unchanged on the drop-in layer",
+           "config": "D (config/config.txt)", "frames_decoded": len(ours),
+           "frames_written": len(res) // pay,
+           "frames_payload_exact": sum(res[i * pay:(i + 1) * pay] in chunks for i in range(len(res) // pay)),
+           "median_us": statistics.median(ours) * 1e6 if ours else None,
+           "p10_us": sorted(ours)[len(ours) // 10] * 1e6 if ours else None,
+           "p90_us": sorted(ours)[9 * len(ours) // 10] * 1e6 if ours else None,
+           "refill_convert_median_us": statistics.median(refills) * 1e6 if refills else None,
+           # parse_log over the reference's committed LOG.txt (9 430 frame iterations; its
+           # authors' machine, FFTW on the CPU), evaluated in the build container
+           "reference_LOG_txt_median_us": 238.42,
+           "reference_note": "the reference's committed LOG.txt (its authors' machine, FFTW, CPU)"}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
