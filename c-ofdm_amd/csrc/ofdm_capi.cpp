@@ -158,6 +158,7 @@ struct ofdm_ctx {
     hipStream_t h_frames_stream = nullptr;  // stream of the last copy out of h_frames
     bool h_frames_used = false;
     int* d_queue = nullptr;        // walker chunk counter (zero between calls)
+    int* d_rxq = nullptr;          // rx dynamic-frame counters {next, done}, zero between launches
     bool queue_zero = false;       // the last call's compaction resets it ...
     hipEvent_t ev_qreset = nullptr;  // ... when this event completes
     hipEvent_t ev_walk = nullptr;  // walk records landed in h_walk
@@ -311,6 +312,7 @@ int ofdm_destroy(ofdm_ctx* c)
     for (auto* g : {&c->h_walk, &c->h_frames})
         if (g->p) (void)hipHostFree(g->p);
     if (c->d_queue) (void)hipFree(c->d_queue);
+    if (c->d_rxq) (void)hipFree(c->d_rxq);
     if (c->ev_qreset) (void)hipEventDestroy(c->ev_qreset);
     if (c->ev_walk) (void)hipEventDestroy(c->ev_walk);
     if (c->ev_wdone) (void)hipEventDestroy(c->ev_wdone);
@@ -572,6 +574,14 @@ int ofdm_create(const ofdm_params* params, int device, ofdm_ctx** out)
             return rc;
         }
     }
+    // rx dynamic-frame counters: zero now, and left zero by every rx launch
+    hipError_t qe = hipMalloc((void**)&c->d_rxq, 2 * sizeof(int));
+    if (qe == hipSuccess) qe = hipMemset(c->d_rxq, 0, 2 * sizeof(int));
+    if (qe == hipSuccess) qe = hipDeviceSynchronize();
+    if (qe != hipSuccess) {
+        ofdm_destroy(c);
+        return hip_fail(qe, "rx frame counters");
+    }
     *out = c;
     return OFDM_OK;
 }
@@ -801,6 +811,7 @@ static int rx_demod_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, siz
     a.k = c->k;
     a.bytes_per_frame = c->geo.bytes_per_frame;
     a.pilot_ampl = (double)c->p.pilot_ampl / 1000;
+    a.queue = c->d_rxq;
     const bool fits = c->S <= ofdm::RX_SMAX && c->D <= ofdm::RX_DPT * (c->N / 8);
     if (!fits) {
         if (c->D > ofdm::RX_DPT * (c->N / 8))
@@ -895,6 +906,7 @@ int ofdm_fft_read(ofdm_ctx* c, const double* fft_buf, size_t nframes, double* re
     a.k = c->k;
     a.bytes_per_frame = c->geo.bytes_per_frame;
     a.pilot_ampl = (double)c->p.pilot_ampl / 1000;
+    a.queue = c->d_rxq;
     if (!(c->S <= ofdm::RX_SMAX && c->D <= ofdm::RX_DPT * (c->N / 8))) a.ystage = a.constell;
     hipError_t e = ofdm::launch_rx(c->logn, a, (hipStream_t)stream, nullptr);
     if (e != hipSuccess) return hip_fail(e, "fft_read launch");
@@ -1327,6 +1339,7 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
             ra.k = c->k;
             ra.bytes_per_frame = c->geo.bytes_per_frame;
             ra.pilot_ampl = (double)c->p.pilot_ampl / 1000;
+            ra.queue = c->d_rxq;
             e2 = ofdm::launch_rx(c->logn, ra, st, nullptr);
             if (e2 != hipSuccess) return hip_fail(e2, "stream rx launch");
         }

@@ -62,6 +62,7 @@ struct RxArgs {
     const long* starts;         // nullable
     long start_off;
     const long* count;          // nullable: frames beyond min(*count, nframes) are skipped
+    int* queue;                 // nullable: {next, done} counters (zero; left zero) for dynamic frames
     const double* corr;
     int S, D, P, seg, cp, k;
     long bytes_per_frame;

@@ -21,6 +21,8 @@
 #include "ofdm_fft.hpp"
 #include "ofdm_internal.hpp"
 
+#include <type_traits>
+
 namespace ofdm {
 
 // ------------------------------------------------------------------ helpers
@@ -44,6 +46,18 @@ __device__ __forceinline__ int symbol_bits(const uint8_t* __restrict__ b, long n
 // The clamp is v_max/v_min: equal to the reference's compare chain for every
 // non-NaN value; a NaN (degenerate all-zero pilots) decides 0 either way
 // (chain: cvt(NaN) = 0; min/max: clamps to -1, then uint8(0.5) = 0).
+// decide() as a select (no branch on k): the same value for every k.
+__device__ __forceinline__ int decide_select(double2 z, int k, double s1, int m)
+{
+    const double re = __builtin_fmin(__builtin_fmax(z.x, -1.0), 1.0);
+    const double im = __builtin_fmin(__builtin_fmax(z.y, -1.0), 1.0);
+    const int ire = (uint8_t)(int)add_rn(mul_rn(add_rn(re, 1.0), s1), 0.5);
+    const int iim = (uint8_t)(int)add_rn(mul_rn(add_rn(im, 1.0), s1), 0.5);
+    const int qam = (ire | (iim * m)) & 0xff;
+    const int bpsk = (z.x + z.y) > 0.0;
+    return k == 1 ? bpsk : qam;
+}
+
 __device__ __forceinline__ int decide(double2 z, int k, double s1, int m)
 {
     if (k == 1) return (z.x + z.y) > 0.0;
@@ -149,6 +163,19 @@ __device__ __forceinline__ void store_nt(double2* p, double2 v)
 {
     nt_double2 w = {v.x, v.y};
     __builtin_nontemporal_store(w, reinterpret_cast<nt_double2*>(p));
+}
+
+// A global load the compiler's wait-count pass does not track: issued and
+// waited for (vmcnt(0)) inside one asm block. For rare paths (e.g. channel
+// carriers that do not fit LDS) inside code that otherwise issues only
+// stores: a tracked load there makes the pass put `s_waitcnt vmcnt(0)` in
+// front of every later store that reuses its registers, which serialises the
+// epilogue's stores behind each other and behind the next frame's prefetch.
+__device__ __forceinline__ double2 load_untracked(const double2* p)
+{
+    double2 v;
+    asm volatile("global_load_dwordx4 %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+    return v;
 }
 
 __device__ __forceinline__ double2 load_nt(const double2* p)
@@ -532,6 +559,13 @@ __device__ __forceinline__ double2 stage_get(const void* stage, int e)
     }
 }
 
+#ifdef OFDM_RX_PROF  // timing experiment only: per-workgroup rx phase clocks (wave 0)
+__device__ unsigned long long g_rx_prof[2 * 4096 * 8];
+#define RPROF(...) __VA_ARGS__
+#else
+#define RPROF(...)
+#endif
+
 template <int LOGN, bool STAGED, bool I16, bool SYNC>
 __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
 {
@@ -554,7 +588,25 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
     // frames to process: a.nframes, or fewer when the count is device-side
     // (speculative stream decode); uniform early exit before any prefetch
     const long nfr = a.count ? min(*a.count, a.nframes) : a.nframes;
-    if ((long)blockIdx.x >= nfr) return;
+    // Dynamic frames (a.queue): a workgroup's first frame is its blockIdx,
+    // later ones come from a counter, so workgroups that run faster (CU and
+    // memory-channel placement make them differ by ~15%) take more frames and
+    // the kernel ends with the mean workgroup, not the slowest. The last
+    // workgroup to leave zeroes the counters for the next launch.
+    auto leave = [&]() {
+        if (a.queue && threadIdx.x == 0) {
+            __threadfence();
+            if (atomicAdd(a.queue + 1, 1) == (int)gridDim.x - 1) {
+                a.queue[0] = 0;
+                a.queue[1] = 0;
+            }
+        }
+    };
+    if ((long)blockIdx.x >= nfr) {
+        leave();
+        return;
+    }
+    int* qslot = reinterpret_cast<int*>(red + 16);  // the next frame from the queue (red[0..7]: reductions)
 
     // table loads first, then symbol 0 of the first frame: every prologue wait
     // below is a counted vmcnt that leaves the symbol prefetch in flight
@@ -570,12 +622,8 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
 #pragma unroll
     for (int i = 0; i < RX_DPT; ++i) pk[i] = a.tab.rx_pack[t0 + T * i];
     const int pbin = a.tab.pilot_swz[t0];
-    long fl = blockIdx.x;  // frames in processing order (f: the frame itself)
-#ifdef OFDM_RX_REV  // timing experiment only: frames in reverse order
-    auto frame_of = [&](long l) { return nfr - 1 - l; };
-#else
+    long fl = blockIdx.x;  // this workgroup's frame
     auto frame_of = [&](long l) { return l; };
-#endif
     SymbolRegs<LOGN, I16> pf;
     // sample offset of frame g's first message body (CP strip, Frame.hpp:278-279)
     auto body0 = [&](long g) { return SYNC ? a.starts[g] + a.start_off : g * a.frame_stride + a.cp; };
@@ -584,13 +632,15 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
     lds_barrier();  // twiddle table visible: fft_pp reads a pass's twiddles before its barrier
 
     unsigned long long errs = 0;
+    RPROF(unsigned long long p_s0 = 0, p_pf = 0, p_fft = 0, p_epi = 0, p_nf = 0, p_gain = 0, p_emit = 0, p_pack = 0;
+          const unsigned long long p_c0 = clock64(); const unsigned long long p_w0 = wall_clock64();)
 
     // Persistent over frames (grid <= 2 workgroups per CU): the next frame's
     // symbol 0 is fetched (LDS-DMA into bufB) while this frame's epilogue
     // runs, so HBM reads do not stop between frames, and the tables are
     // loaded once per workgroup.
 #pragma unroll 1
-    for (; fl < nfr; fl += fstep) {
+    for (long fnext; fl < nfr; fl = fnext) {
         const long f = frame_of(fl);
         // Opaque per-frame copies of the thread index, the carrier tables and
         // the geometry: everything derived from them is recomputed per frame
@@ -618,14 +668,18 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
 #pragma unroll 1
         for (int s = 0; s < S; ++s) {
             double2 v[8];
+            RPROF(const unsigned long long p_a = clock64();)
             if (s == 0) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of symbol 0 landed
+                RPROF(p_s0 += clock64() - p_a;)
 #pragma unroll
                 for (int i = 0; i < 8; ++i) v[i] = stage_get<LOGN, I16>(bufB, t + T * i);
             } else {
+                RPROF(asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); p_pf += clock64() - p_a;)
 #pragma unroll
                 for (int i = 0; i < 8; ++i) v[i] = pf.get(i);
             }
+            RPROF(const unsigned long long p_b = clock64();)
             // SYNC: the phase ramp is applied before the next symbol's
             // prefetch is issued, so its sincos temporaries are not live
             // beside the 8 prefetch registers (which spilled at N = 512)
@@ -682,7 +736,9 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
                     default: break;
                 }
             }
+            RPROF(p_fft += clock64() - p_b;)
         }
+        RPROF(const unsigned long long p_e = clock64();)
         lds_barrier();  // pilots of the last symbol visible; every thread is done reading bufB
         // The channel carriers go to LDS (bufA past the decisions) by DMA
         // issued ahead of the next frame's symbol 0: read per point from HBM
@@ -692,8 +748,10 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
         double2* chl = reinterpret_cast<double2*>(reinterpret_cast<char*>(bufA) + dec_b);
         const bool chan_lds = chan && dec_b + D * 16 <= N * 16;  // uniform
         if (chan_lds) dma_chan<LOGN>(chan, D, chl, t);
-        const bool next = fl + fstep < nfr;
-        if (next) dma_symbol<LOGN, I16>(a, body0(frame_of(fl + fstep)), bufB, t);
+        // the next frame: asked for now, its answer awaited after the gains
+        // (the register holding it is live across the gains only)
+        int qv = 0;
+        if (a.queue && t == 0) qv = atomicAdd(a.queue, 1);
 
         // phys_pilot_ampl = sum |pilot| / (P*S*pilot_ampl)   (Frame.cpp:76-80)
         double acc = 0.0;
@@ -710,13 +768,14 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
             const double2 g = cdiv_exact(make_double2(1.0, 0.0), coef);
             gain[i] = make_double2(g.x / phys, g.y / phys);
         }
-        if (chan_lds) {  // the channel DMA landed (the 8 symbol-0 transfers may still fly)
-            if (next)
-                asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-            else
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+        if (chan_lds) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the channel DMA landed
+        if (a.queue && t == 0) *qslot = qv;
         lds_barrier();
+        // symbol 0 of the next frame streams into bufB (free since the pilot
+        // barrier) behind the emit and the packing
+        fnext = a.queue ? fstep + __builtin_amdgcn_readfirstlane(*qslot) : fl + fstep;  // uniform: an SGPR
+        if (fnext < nfr) dma_symbol<LOGN, I16>(a, body0(frame_of(fnext)), bufB, t);
+        RPROF(const unsigned long long p_g = clock64(); p_gain += p_g - p_e;)
 
         auto emit = [&](int s, int i, double2 yv) {
             // opaque: the per-point addresses are computed here, not hoisted
@@ -728,12 +787,68 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
             (void)chan;
 #else
             if (chan) {
-                const double2 cv = chan_lds ? chl[d] : chan[d];
+                const double2 cv = chan_lds ? chl[d] : load_untracked(chan + d);
                 o = a.chan_recip ? cmul_exact(o, cv) : cdiv_exact(o, cv);
             }
 #endif
+#ifdef OFDM_RX_NOCSTORE  // timing experiment only: no constellation stores
+            if (a.constell && o.x == 12345.678) store_nt(a.constell + (f * S + s) * D + d, o);
+#else
+            if (a.constell) store_nt(a.constell + (f * S + s) * D + d, o);
+#endif
+            dec[whole_frame_dec ? s * D + d : d] = (uint8_t)decide(o, a.k, s1, m);
+        };
+
+        // One symbol's RX_DPT points of the register window. Without a
+        // channel (the common case) the group's gain loads are issued first
+        // and the points then computed, stored and decided; the uniform
+        // branches are taken once per group, so the points' LDS latencies
+        // overlap. With a channel, one point at a time (register pressure).
+        auto emit_point = [&](int s, int i, double2 yv) {
+            // opaque: the per-point addresses are computed here, not hoisted
+            // out of the emit loop and held (32 of them) across it
+            int d = t + T * i, gi = s * P + (pk[i] >> 16);
+            asm volatile("" : "+v"(d), "+v"(gi));
+            double2 o = cmul_exact(yv, gain[gi]);
+#ifndef OFDM_RX_NOCHAN  // timing experiment only: no channel correction
+            const double2 cv = chan_lds ? chl[d] : load_untracked(chan + d);
+            o = a.chan_recip ? cmul_exact(o, cv) : cdiv_exact(o, cv);
+#endif
             if (a.constell) store_nt(a.constell + (f * S + s) * D + d, o);
             dec[whole_frame_dec ? s * D + d : d] = (uint8_t)decide(o, a.k, s1, m);
+        };
+        // Without a channel (the common case) a group is straight-line code:
+        // the output branch is taken once per group and the decision is
+        // branch-free, so the scheduler can overlap the points' LDS reads.
+        auto emit_plain = [&](int s, const double2 (&yw)[RX_DPT], auto with_store) {
+            double2* cbase = a.constell + (f * S + s) * D;
+#pragma unroll
+            for (int i = 0; i < RX_DPT; ++i) {
+                int d = t + T * i, gi = s * P + (pk[i] >> 16);
+                asm volatile("" : "+v"(d), "+v"(gi));  // opaque: not hoisted and held
+                if (d < D) {
+                    const double2 o = cmul_exact(yw[i], gain[gi]);
+                    if constexpr (decltype(with_store)::value) {
+#ifdef OFDM_RX_NOCSTORE  // timing experiment only: no constellation stores
+                        if (o.x == 12345.678) store_nt(cbase + d, o);
+#else
+                        store_nt(cbase + d, o);
+#endif
+                    }
+                    dec[whole_frame_dec ? s * D + d : d] = (uint8_t)decide_select(o, a.k, s1, m);
+                }
+            }
+        };
+        auto emit_group = [&](int s, const double2 (&yw)[RX_DPT]) {
+            if (SYNC || chan) {  // the stream decode always has its channel
+#pragma unroll
+                for (int i = 0; i < RX_DPT; ++i)
+                    if (t + T * i < D) emit_point(s, i, yw[i]);
+            } else if (a.constell) {
+                emit_plain(s, yw, std::true_type{});
+            } else {
+                emit_plain(s, yw, std::false_type{});
+            }
         };
 
         auto pack = [&](long jb0, long jb1, long dbase) {
@@ -779,11 +894,11 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
 #pragma unroll 1
             for (int w = 0; w < S; ++w) {
                 switch (w) {
-#define OFDM_RX_EMIT(W)                                                                   \
-    case W:                                                                               \
-        if constexpr (W < SW) {                                                           \
-            _Pragma("unroll") for (int i = 0; i < RX_DPT; ++i) if (t + T * i < D) emit(w, i, y[W][i]); \
-        }                                                                                 \
+#define OFDM_RX_EMIT(W)                 \
+    case W:                             \
+        if constexpr (W < SW) {         \
+            emit_group(w, y[W]);        \
+        }                               \
         break;
                     OFDM_RX_EMIT(0) OFDM_RX_EMIT(1) OFDM_RX_EMIT(2) OFDM_RX_EMIT(3)
                     OFDM_RX_EMIT(4) OFDM_RX_EMIT(5) OFDM_RX_EMIT(6) OFDM_RX_EMIT(7)
@@ -791,17 +906,22 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
                     default: break;
                 }
             }
+            RPROF(p_emit += clock64() - p_g;)
             lds_barrier();
+            RPROF(const unsigned long long p_k = clock64();)
             if (by_word)
                 pack_words();
             else
                 pack(0, bpf, 0);
+            RPROF(p_pack += clock64() - p_k;)
         } else {
             const long bps = (long)D * a.k / 8;  // bytes per symbol (host checks D*k % 8 == 0)
             for (int s = 0; s < S; ++s) {
+                double2 yst[RX_DPT];
 #pragma unroll
                 for (int i = 0; i < RX_DPT; ++i)
-                    if (t + T * i < D) emit(s, i, a.ystage[(f * S + s) * D + t + T * i]);
+                    yst[i] = t + T * i < D ? a.ystage[(f * S + s) * D + t + T * i] : make_double2(0.0, 0.0);
+                emit_group(s, yst);
                 lds_barrier();
                 if (!whole_frame_dec) {
                     pack(s * bps, (s + 1) * bps, 0);
@@ -811,11 +931,20 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
             if (whole_frame_dec) pack(0, bpf, 0);
         }
         lds_barrier();  // dec / pil / gain / red are rewritten by the next frame
+        RPROF(p_epi += clock64() - p_e; ++p_nf;)
     }
+    RPROF(if (t0 == 0 && blockIdx.x < 4096) {
+        unsigned long long* q = g_rx_prof + 8 * blockIdx.x;
+        q[0] = p_s0; q[1] = p_pf; q[2] = p_fft; q[3] = p_epi; q[4] = p_nf; q[5] = clock64() - p_c0;
+        q[6] = p_w0; q[7] = wall_clock64();
+        unsigned long long* u = g_rx_prof + 8 * 4096 + 8 * blockIdx.x;
+        u[0] = p_gain; u[1] = p_emit; u[2] = p_pack;
+    })
     if (a.bit_errors) {
         errs = block_sum_u64<T>(errs, red);
         if (t0 == 0 && errs) atomicAdd(a.bit_errors, errs);
     }
+    leave();
 }
 
 // ------------------------------------------------------------------ demap / map
@@ -893,6 +1022,15 @@ __global__ void f64_to_i16_kernel(const double2* __restrict__ in, long n, double
         out[i] = make_short2(to_int16(v.x * mult), to_int16(v.y * mult));
     }
 }
+
+#ifdef OFDM_RX_PROF
+extern "C" int ofdm_rx_prof(unsigned long long* out)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rx_prof), sizeof(unsigned long long) * 2 * 4096 * 8) == hipSuccess
+               ? 0
+               : -1;
+}
+#endif
 
 // ------------------------------------------------------------------ launchers
 static int num_cus();
