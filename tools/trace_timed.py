@@ -21,7 +21,7 @@ def main():
             continue
         timed = d[-steps:]
         res["kernels"][key] = {
-            "name": next(r["Kernel_Name"] for r in rows if key in r["Kernel_Name"]),
+            "name": next(r["Kernel_Name"] for r in rows if key in r["Kernel_Name"] and int(r["Grid_Size_X"]) > 1024),
             "launches": len(d),
             "avg_all_ms": sum(d) / len(d),
             "avg_timed_ms": sum(timed) / len(timed),
