@@ -452,6 +452,48 @@ __device__ __forceinline__ void fft_regs_active(double2 (&v)[8], int t, const do
     fft_regs_tail_active<LOGN, 1, SIGN>(v, t, lds_tw, lds, active);
 }
 
+// ---------------------------------------------------------------- one wave
+// fft_regs for N = 512 (T = 64) run by ONE wave of a larger workgroup. Within
+// a wave an LDS hand-off needs only the wave's own LDS operations complete
+// (lgkmcnt(0)), not a workgroup barrier, so the other waves stay free (they
+// wait at the caller's next barrier instead of at every pass).
+__device__ __forceinline__ void wave_lds_sync()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+template <int LOGN, int PASS, int SIGN>
+__device__ __forceinline__ void fft_regs_tail_wave(double2 (&v)[8], int t, const double2* __restrict__ lds_tw,
+                                                   double2* __restrict__ lds)
+{
+    using S = FftShape<LOGN>;
+    constexpr int NPASS = S::NPASS8 + (S::REM ? 1 : 0);
+    constexpr bool is8 = PASS < S::NPASS8;
+    constexpr int R = is8 ? 8 : (1 << S::REM);
+    constexpr int NS = 1 << (3 * PASS);
+    constexpr bool LAST = PASS == NPASS - 1;
+    const auto tw = pass_twiddles<LOGN, R, NS, SIGN>(t, lds_tw);
+    wave_lds_sync();  // previous pass fully written
+    lds_load8<LOGN>(v, t, lds);
+    if constexpr (LAST) {
+        stockham_apply<LOGN, R, NS, SIGN, false>(v, t, tw, lds);
+    } else {
+        wave_lds_sync();  // every lane has read before the image is overwritten
+        stockham_apply<LOGN, R, NS, SIGN>(v, t, tw, lds);
+        fft_regs_tail_wave<LOGN, PASS + 1, SIGN>(v, t, lds_tw, lds);
+    }
+}
+
+// On entry v[i] = x[t + 64*i] (t = lane); on exit v[i] = X[t + 64*i].
+template <int LOGN, int SIGN>
+__device__ __forceinline__ void fft_regs_wave(double2 (&v)[8], int t, const double2* __restrict__ lds_tw,
+                                              double2* __restrict__ lds)
+{
+    static_assert(LOGN == 9, "one wave = N/8 = 64 threads");
+    stockham_pass<LOGN, 8, 1, SIGN>(v, t, lds_tw, lds);
+    fft_regs_tail_wave<LOGN, 1, SIGN>(v, t, lds_tw, lds);
+}
+
 // ---------------------------------------------------------------- ping-pong
 // Same transform over two LDS images: pass p writes buf[(start + p) & 1] and
 // pass p+1 reads it, so one barrier per pass suffices (a buffer is only

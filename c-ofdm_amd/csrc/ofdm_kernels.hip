@@ -748,8 +748,17 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
         double2* chl = reinterpret_cast<double2*>(reinterpret_cast<char*>(bufA) + dec_b);
         const bool chan_lds = chan && dec_b + D * 16 <= N * 16;  // uniform
         if (chan_lds) dma_chan<LOGN>(chan, D, chl, t);
-        // the next frame: asked for now, its answer awaited after the gains
-        // (the register holding it is live across the gains only)
+        // Static frame order (no queue; the stream decode): the next frame's
+        // symbol 0 streams into bufB (free since the pilot barrier) from here,
+        // behind the channel carriers, so it overlaps the gains as well.
+        // With the queue the next frame is asked for now, its answer awaited
+        // after the gains (the register holding it is live across the gains
+        // only), and its DMA issued after them.
+        const bool early = !a.queue;  // uniform
+        if (early) {
+            fnext = fl + fstep;
+            if (fnext < nfr) dma_symbol<LOGN, I16>(a, body0(frame_of(fnext)), bufB, t);
+        }
         int qv = 0;
         if (a.queue && t == 0) qv = atomicAdd(a.queue, 1);
 
@@ -768,36 +777,21 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
             const double2 g = cdiv_exact(make_double2(1.0, 0.0), coef);
             gain[i] = make_double2(g.x / phys, g.y / phys);
         }
-        if (chan_lds) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the channel DMA landed
+        if (chan_lds) {  // the channel DMA landed (the 8 symbol-0 transfers issued after it may still fly)
+            if (early && fnext < nfr)
+                asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         if (a.queue && t == 0) *qslot = qv;
         lds_barrier();
-        // symbol 0 of the next frame streams into bufB (free since the pilot
-        // barrier) behind the emit and the packing
-        fnext = a.queue ? fstep + __builtin_amdgcn_readfirstlane(*qslot) : fl + fstep;  // uniform: an SGPR
-        if (fnext < nfr) dma_symbol<LOGN, I16>(a, body0(frame_of(fnext)), bufB, t);
+        if (!early) {
+            // symbol 0 of the next frame streams into bufB behind the emit and
+            // the packing
+            fnext = fstep + __builtin_amdgcn_readfirstlane(*qslot);  // uniform: an SGPR
+            if (fnext < nfr) dma_symbol<LOGN, I16>(a, body0(frame_of(fnext)), bufB, t);
+        }
         RPROF(const unsigned long long p_g = clock64(); p_gain += p_g - p_e;)
-
-        auto emit = [&](int s, int i, double2 yv) {
-            // opaque: the per-point addresses are computed here, not hoisted
-            // out of the emit loop and held (32 of them) across it
-            int d = t + T * i, gi = s * P + (pk[i] >> 16);
-            asm volatile("" : "+v"(d), "+v"(gi));
-            double2 o = cmul_exact(yv, gain[gi]);
-#ifdef OFDM_RX_NOCHAN  // timing experiment only: no channel correction
-            (void)chan;
-#else
-            if (chan) {
-                const double2 cv = chan_lds ? chl[d] : load_untracked(chan + d);
-                o = a.chan_recip ? cmul_exact(o, cv) : cdiv_exact(o, cv);
-            }
-#endif
-#ifdef OFDM_RX_NOCSTORE  // timing experiment only: no constellation stores
-            if (a.constell && o.x == 12345.678) store_nt(a.constell + (f * S + s) * D + d, o);
-#else
-            if (a.constell) store_nt(a.constell + (f * S + s) * D + d, o);
-#endif
-            dec[whole_frame_dec ? s * D + d : d] = (uint8_t)decide(o, a.k, s1, m);
-        };
 
         // One symbol's RX_DPT points of the register window. Without a
         // channel (the common case) the group's gain loads are issued first

@@ -1078,6 +1078,64 @@ __device__ __forceinline__ double2 stream_sample_in(const A& a, long j)
     return a.iq[j];
 }
 
+// Eight samples x[base + lane + 64*i] (zero where lane + 64*i >= W or the
+// index is outside [0, n)), all eight loads issued before any is used:
+// clamped addresses and selects, no per-sample branch (a branch around each
+// load, or a use inside it, makes each load wait for the one before).
+template <class A>
+__device__ __forceinline__ void load8_window(const A& a, long base, int lane, int W, double2 (&v)[8])
+{
+    long j[8];
+    bool ok[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const long q = base + lane + 64 * i;
+        ok[i] = lane + 64 * i < W && q >= 0 && q < a.n;
+        j[i] = ok[i] ? q : 0;
+    }
+    if (a.iq16) {  // uniform
+        const int* p = reinterpret_cast<const int*>(a.iq16);
+        int w[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w[i] = p[j[i]];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            v[i] = ok[i] ? make_double2((double)(int)(short)(w[i] & 0xffff), (double)(w[i] >> 16))
+                         : make_double2(0.0, 0.0);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = a.iq[j[i]];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (!ok[i]) v[i] = make_double2(0.0, 0.0);
+    }
+}
+
+// x[base + T*i], i < 8, all in [0, n) when `live` (else zeros), loads
+// issued together (the int16 loads waited one by one behind per-sample branches).
+template <int T, class A>
+__device__ __forceinline__ void load8_block(const A& a, long base, bool live, double2 (&v)[8])
+{
+    const long b0 = live ? base : 0;
+    if (a.iq16) {  // uniform
+        const int* p = reinterpret_cast<const int*>(a.iq16) + b0;
+        int w[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w[i] = p[T * i];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            v[i] = live ? make_double2((double)(int)(short)(w[i] & 0xffff), (double)(w[i] >> 16))
+                        : make_double2(0.0, 0.0);
+    } else {
+        const double2* p = a.iq + b0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = p[T * i];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (!live) v[i] = make_double2(0.0, 0.0);
+    }
+}
+
 // PREAMBLE_FORM::find_preamble from s: first lag with norm > 1 and
 // |sum_j x[s+i+j] c_j| / sqrt(norm) > level (Frame.cpp:338-378), INT_MAX if
 // none. Exact form: the running energy is the reference's serial recurrence
@@ -1219,134 +1277,160 @@ __device__ int walk_preamble(const WalkArgs& a, long s, double2* xs, const doubl
     return found;
 }
 
-// FFT form of the certified search (cycles + L <= M = WALK_FFT_M): all lags'
-// correlations at once as e = IFFT(FFT(x) . tspec) / M (linear correlation:
-// no wrap for i + j < cycles + L <= M), energies as prefix sums. The FFT
-// result differs from the reference's in-order sum by at most
+// FFT form of the certified search, run by wave 0 alone over windows of
+// Q = M - L + 1 lags (M = WALK_FFT_M = 512): a window's correlations are
+// e = IFFT(FFT(x) . tspec) / M over its Q + L - 1 samples (linear correlation:
+// no wrap), its energies prefix sums. Lags are decided in order and the
+// search stops at the window holding the first lag that is not a certain
+// FAIL, so the usual step (preamble ~T2sin_size after the hit) transforms one
+// window of 512 samples. The FFT result differs from the reference's in-order
+// sum by at most
 //   |e^ - e| <= 1024 u ||x||_2 max|tspec|   (~10x the FFT-convolution bound,
 // (2 c log2 M + 1) u ||x|| ||tspec||_inf), and a window energy from two prefix
-// sums from the serial recurrence by (2L + 2i + 8) u (M + s_i) + (4R + 64) u P,
-// so a lag clear of both thresholds by those margins is decided as the
-// reference decides it; the first lag that is not a certain FAIL must be a
-// certain PASS, else the exact search runs. Uses 128 threads for the
-// transforms (fft_block_active); buf: M entries, P: cycles + L doubles.
-__device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double* P, const double2* tw_m,
-                                 double* scr, int* best, int* unsure, double2* xs, double* E, double* normv, int t)
+// sums from the serial recurrence by (2L + 2i + 8) u (M + s_i) + (4R + 64) u P
+// (i: the lag from the search start; M: the largest window sum and sample
+// energy of every lag so far), so a lag clear of both thresholds by those
+// margins is decided as the reference decides it; the first lag that is not a
+// certain FAIL must be a certain PASS, else the exact search runs. The other
+// waves wait at the closing barrier (the transforms synchronise within the
+// wave only). buf: M entries, P: M doubles (both in the search scratch).
+__device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double* P, const double2* tw_m, int* res,
+                                 double2* xs, double* E, double* normv, int* best, int t)
 {
     constexpr double U = 0x1.0p-53;
-    constexpr int LM = WALK_FFT_LOGM, M = WALK_FFT_M, TM = M / 8;
-    const int L = a.L, C = a.cycles, W = C + L;
-    const bool active = t < TM;
-    const bool whole = s >= 0 && s + W <= a.n;  // uniform: the window needs no bounds tests
-    WPROF(const unsigned long long q0 = clock64();)
-    double2 v[8];
-    double emax = 0.0;
+    constexpr int LM = WALK_FFT_LOGM, M = WALK_FFT_M, R = M / 64;
+    static_assert(M == 512, "one wave: M/8 = 64 lanes");
+    WPROF(const unsigned long long q0 = clock64(); unsigned long long q1 = q0, q2 = q0, q3 = q0;)
+    if (t < 64) {  // wave 0
+        const int L = a.L, C = a.cycles, Q = M - L + 1;
+        double mrun = 0.0, erun = 0.0;  // largest window sum / sample energy of the windows so far
+        int out = INT_MAX;              // first certain PASS; -2 - lag: the first undecided lag
+        constexpr double inv_m = 1.0 / M;
+        const double lev2 = a.pr_level * a.pr_level;
+        for (int i0 = 0; i0 < C && out == INT_MAX; i0 += Q) {  // uniform
+            // opaque per-window copy of the lane: the addresses derived from
+            // it are recomputed here, not hoisted out of the walk and held
+            // live (spilled) across it
+            int lane;
+            asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(t));
+            const int nl = min(Q, C - i0), W = nl + L - 1;
+            const long s0 = s + i0;
+            double2 v[8];
+            load8_window(a, s0, lane, W, v);
+            double emax = 0.0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int k = t + TM * i;
-        v[i] = make_double2(0.0, 0.0);
-        if (active && k < W) {
-            v[i] = whole ? stream_sample_in(a, s + k) : stream_sample(a, s + k);
-            const double e2 = add_rn(mul_rn(v[i].x, v[i].x), mul_rn(v[i].y, v[i].y));
-            P[k] = e2;
-            emax = fmax(emax, e2);
+            for (int i = 0; i < 8; ++i) {
+                const int k = lane + 64 * i;
+                const double e2 = add_rn(mul_rn(v[i].x, v[i].x), mul_rn(v[i].y, v[i].y));
+                if (k < W) P[k] = e2;
+                emax = fmax(emax, e2);
+            }
+            wave_lds_sync();  // P visible across the wave
+            // inclusive prefix sums of P: lane owns entries R*lane .. R*lane + R-1
+            double ptot;
+            {
+                double pl[R], loc = 0.0;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int k = R * lane + r;
+                    pl[r] = k < W ? P[k] : 0.0;
+                    loc += pl[r];
+                }
+                double inc = loc;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const double y = __shfl_up(inc, o);
+                    if (lane >= o) inc += y;
+                }
+                ptot = __shfl(inc, 63);
+                double run = inc - loc;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int k = R * lane + r;
+                    run += pl[r];
+                    if (k < W) P[k] = run;
+                }
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) emax = fmax(emax, __shfl_xor(emax, o));
+            fft_regs_wave<LM, -1>(v, lane, tw_m, buf);  // X[lane + 64 i] (its LDS syncs publish P too)
+            WPROF(q1 = clock64();)
+            // Y = X . tspec (L2-resident table). The table address comes from
+            // an opaque copy of the lane here: hoisted out of the walk loop,
+            // the eight 64-bit addresses stayed live (and spilled) across it
+            {
+                int ln;
+                asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+                const double2* tp = a.tspec + ln;
+                double2 ts[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) ts[i] = tp[64 * i];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v[i] = cmul(v[i], ts[i]);
+            }
+            WPROF(q2 = clock64();)
+            fft_regs_wave<LM, +1>(v, lane, tw_m, buf);  // v[j] = M e_{i0 + lane + 64 j} (P final: synced inside)
+            WPROF(q3 = clock64();)
+            // parked in LDS (each lane its own entries, after its last read of
+            // the image), so the decisions below run as a rolled loop
+#pragma unroll
+            for (int j = 0; j < 8; ++j) buf[lane + 64 * j] = v[j];
+            // the largest window sum of this window's lags
+            double mloc = 0.0;
+#pragma unroll 1
+            for (int j = 0; j < 8; ++j) {
+                const int r = lane + 64 * j;
+                if (r < nl) mloc = fmax(mloc, P[r + L - 1] - (r ? P[r - 1] : 0.0));
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) mloc = fmax(mloc, __shfl_xor(mloc, o));
+            mrun = fmax(mrun, mloc);
+            erun = fmax(erun, emax);
+            const double Mall = (mrun + erun) * 1.0625;
+            const double scan_err = (4.0 * R + 64.0) * U * ptot;
+            const double ef = 1024.0 * U * sqrt(ptot * 1.0625) * a.tspec_max;
+#pragma unroll 1
+            for (int j = 0; j < 8; ++j) {
+                const int r = lane + 64 * j, i = i0 + r;
+                int d = 0;  // 0 = certain FAIL, 1 = certain PASS, 2 = uncertain
+                if (r < nl) {
+                    const double sn = P[r + L - 1] - (r ? P[r - 1] : 0.0);
+                    const double B = (2.0 * L + 2.0 * i + 8.0) * U * (Mall + sn) * 1.25 + scan_err;
+                    if (sn + B > 1.0) {  // else n_i <= 1 for sure
+                        // the ratio tests squared (one sqrt, no hypot or division): the
+                        // 32U / 16U slack factors cover these roundings and the
+                        // reference's own (hypot, sqrt, divide)
+                        const double2 e = buf[r];
+                        const double ae = sqrt(e.x * e.x + e.y * e.y) * inv_m;
+                        const double hi = (ae + ef) * (1.0 + 32.0 * U);
+                        const double lo = fmax(ae - ef, 0.0) * (1.0 - 32.0 * U);
+                        if (!(hi * hi <= lev2 * fmax(sn - B, 0x1.0p-1000) * (1.0 - 16.0 * U)))
+                            d = (sn - B > 1.0 && lo * lo > lev2 * (sn + B) * (1.0 + 16.0 * U)) ? 1 : 2;
+                    }
+                }
+                const unsigned long long hitm = __ballot(d != 0);
+                if (hitm) {  // uniform: the lowest such lane is the first undecided-or-PASS lag
+                    const int l0 = __ffsll((long long)hitm) - 1;
+                    const int d0 = __shfl(d, l0);
+                    const int lag = i0 + 64 * j + l0;
+                    out = d0 == 1 ? lag : -2 - lag;
+                    break;
+                }
+            }
+            wave_lds_sync();  // every lane is done with buf / P before the next window overwrites them
         }
+        if (t == 0) *res = out;
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) emax = fmax(emax, __shfl_xor(emax, o));
-    if ((t & 63) == 0) scr[t >> 6] = emax;
-    if (t == 0) {
-        *best = INT_MAX;
-        *unsure = INT_MAX;
-    }
-    // X, its last pass in registers: v[i] = X[t + TM*i] (barriers: P and scr visible)
-    fft_regs_active<LM, -1>(v, t, tw_m, buf, active);
-    WPROF(const unsigned long long q1 = clock64();)
-
-    // inclusive prefix sums of P: thread t owns R consecutive entries
-    const int R = (W + WALK_THREADS - 1) / WALK_THREADS;
-    double loc = 0.0;
-    for (int r = 0; r < R; ++r) {
-        const int k = t * R + r;
-        if (k < W) loc += P[k];
-    }
-    double inc = loc;  // wave inclusive scan
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const double y = __shfl_up(inc, o);
-        if ((t & 63) >= o) inc += y;
-    }
-    if ((t & 63) == 63) scr[8 + (t >> 6)] = inc;
-    // Y = X . tspec, into registers for the inverse transform
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int k = t + TM * i;
-        if (active) v[i] = cmul(v[i], a.tspec[k]);
-    }
-    lds_barrier();  // the wave totals are visible; every thread is done with the forward image
-    double run = inc - loc;
-    for (int w = 0; w < (t >> 6); ++w) run += scr[8 + w];
-    for (int r = 0; r < R; ++r) {
-        const int k = t * R + r;
-        if (k < W) {
-            run += P[k];
-            P[k] = run;
-        }
-    }
-    WPROF(const unsigned long long q2 = clock64();)
-    fft_block_active<LM, +1>(v, t, tw_m, buf, active);  // M e_i at buf[lds_swz(i)] (barriers: P final)
-    WPROF(const unsigned long long q3 = clock64();)
-
-    double eb = scr[0];
-    for (int w = 1; w < WALK_THREADS / 64; ++w) eb = fmax(eb, scr[w]);
-    const double ptot = P[W - 1];
-    // max window sum over all lags
-    double mloc = 0.0;
-    for (int i = t; i < C; i += WALK_THREADS) mloc = fmax(mloc, P[i + L - 1] - (i ? P[i - 1] : 0.0));
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mloc = fmax(mloc, __shfl_xor(mloc, o));
-    if ((t & 63) == 0) scr[12 + (t >> 6)] = mloc;
-    lds_barrier();
-    double mb = scr[12];
-    for (int w = 1; w < WALK_THREADS / 64; ++w) mb = fmax(mb, scr[12 + w]);
-    const double Mall = (mb + eb) * 1.0625;
-    const double scan_err = (4.0 * R + 64.0) * U * ptot;
-    const double ef = 1024.0 * U * sqrt(ptot * 1.0625) * a.tspec_max;
-    constexpr double inv_m = 1.0 / M;
-    const double lev2 = a.pr_level * a.pr_level;
-    for (int i = t; i < C; i += WALK_THREADS) {
-        const double sn = P[i + L - 1] - (i ? P[i - 1] : 0.0);
-        const double2 e = buf[lds_swz(i)];
-        const double B = (2.0 * L + 2.0 * i + 8.0) * U * (Mall + sn) * 1.25 + scan_err;
-        int d;  // 0 = certain FAIL, 1 = certain PASS, 2 = uncertain
-        if (sn + B <= 1.0) {
-            d = 0;  // n_i <= 1 for sure
-        } else {
-            // the ratio tests squared (one sqrt, no hypot or division): the
-            // 32U / 16U slack factors cover these roundings and the
-            // reference's own (hypot, sqrt, divide), so a certain FAIL / PASS
-            // is still one the reference makes (see the bound above)
-            const double ae = sqrt(e.x * e.x + e.y * e.y) * inv_m;
-            const double hi = (ae + ef) * (1.0 + 32.0 * U);
-            const double lo = fmax(ae - ef, 0.0) * (1.0 - 32.0 * U);
-            if (hi * hi <= lev2 * fmax(sn - B, 0x1.0p-1000) * (1.0 - 16.0 * U))
-                d = 0;
-            else
-                d = (sn - B > 1.0 && lo * lo > lev2 * (sn + B) * (1.0 + 16.0 * U)) ? 1 : 2;
-        }
-        if (d) atomicMin(best, i);
-        if (d == 2) atomicMin(unsure, i);
-    }
-    lds_barrier();
-    const int found = *best, un = *unsure;
-    lds_barrier();  // every thread has read best/unsure
+    lds_barrier();  // the answer visible to every wave
+    const int found = *res;
     WPROF(if (t == 0 && blockIdx.x < 8192) {
         unsigned long long* q = g_walk_sub + 8 * blockIdx.x;
         const unsigned long long q4 = clock64();
         q[0] += q1 - q0; q[1] += q2 - q1; q[2] += q3 - q2; q[3] += q4 - q3;
     })
-    if (found != INT_MAX && un == found) {
+    if (found < -1) {  // uniform: a lag within the error bounds of a threshold
         WPROF(if (t == 0) atomicAdd(&g_walk_fallbacks, 1ULL));
+        lds_barrier();  // every wave has read *res (the exact search reuses the scratch)
         return walk_preamble_exact(a, s, xs, a.templ, E, normv, best, t);
     }
     return found;
@@ -1372,7 +1456,7 @@ __global__ void __launch_bounds__(WALK_THREADS, 4) stream_walk_kernel(WalkArgs a
     int* unsure = best + 2;
     double* scr = reinterpret_cast<double*>(best + 4);  // 16 scan / max scratch
     // T2 first-hit block, two slots used alternately (one barrier per scan
-    // step), in scr[4] (the preamble search uses scr[0..3], [8..15]): the
+    // step), in scr[4] (the preamble search's answer is scr[2]): the
     // walker's LDS stays at 4 walkers per CU
     int* bslot = reinterpret_cast<int*>(scr + 4);
     double2* tw_m = reinterpret_cast<double2*>(scr + 16);  // TwLds<WALK_FFT_LOGM> (FFT search)
@@ -1381,7 +1465,7 @@ __global__ void __launch_bounds__(WALK_THREADS, 4) stream_walk_kernel(WalkArgs a
     double2* xs = big;                                  // cycles + L samples (preamble search)
     double* E = reinterpret_cast<double*>(xs + a.cycles + a.L);  // cycles + L energies
     double* normv = E + a.cycles + a.L;                 // cycles running energies (exact fallback)
-    double* P = reinterpret_cast<double*>(big + WALK_FFT_M);  // cycles + L prefix energies (FFT search)
+    double* P = reinterpret_cast<double*>(big + WALK_FFT_M);  // a window's prefix energies (FFT search)
 
     int* qslot = best + 3;  // the chunk taken from the queue
     const int t0 = threadIdx.x;
@@ -1456,8 +1540,7 @@ __global__ void __launch_bounds__(WALK_THREADS, 4) stream_walk_kernel(WalkArgs a
             const long b = base + (long)g * N;
             const bool live = b + N <= a.n;
             double2 v[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) v[i] = live ? stream_sample_in(a, b + tt + T * i) : make_double2(0.0, 0.0);
+            load8_block<T>(a, b + tt, live, v);
             WPROF(const unsigned long long r0 = clock64();)
             // the last pass stays in registers: v[i] = X[tt + T*i], the bins
             // this thread sums (no final LDS write, barrier and re-read); the
@@ -1516,7 +1599,8 @@ __global__ void __launch_bounds__(WALK_THREADS, 4) stream_walk_kernel(WalkArgs a
         if (stop) break;
         WPROF(++p_np;)
         const int lag = (a.tspec && !a.exact_only)
-                            ? walk_preamble_fft(a, hit, big, P, tw_m, scr, best, unsure, xs, E, normv, t)
+                            ? walk_preamble_fft(a, hit, big, P, tw_m, reinterpret_cast<int*>(scr + 2), xs, E, normv,
+                                                best, t)
                             : walk_preamble(a, hit, xs, ctap, E, normv, best, unsure, mred, t);
         WPROF(p_pre += clock64() - p_b;)
         const long pb = (lag == INT_MAX ? -10 : hit + lag) + 1;  // rx.cpp:160
@@ -1569,7 +1653,7 @@ static hipError_t walk_launch_n(const WalkArgs& a, long nblocks, hipStream_t st)
 {
     constexpr int N = 1 << LOGT, T = N / 8, G = WALK_THREADS / T, NW = T >= 64 ? T / 64 : 1;
     const size_t search = sizeof(double2) * ((size_t)a.cycles + a.L) + sizeof(double) * (2 * (size_t)a.cycles + a.L);
-    const size_t fsearch = a.tspec ? sizeof(double2) * WALK_FFT_M + sizeof(double) * ((size_t)a.cycles + a.L) : 0;
+    const size_t fsearch = a.tspec ? (sizeof(double2) + sizeof(double)) * WALK_FFT_M : 0;
     const size_t big = std::max(std::max(sizeof(double2) * (size_t)G * N, search), fsearch);
     const size_t shm = sizeof(double2) * (TwLds<LOGT>::SIZE + G * NW + a.L) + sizeof(double) * 2 * (WALK_THREADS / 64) +
                        16 + sizeof(double) * 16 + sizeof(double2) * TwLds<WALK_FFT_LOGM>::SIZE + big;

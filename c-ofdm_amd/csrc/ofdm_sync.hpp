@@ -100,13 +100,14 @@ struct WalkArgs {
     int* ncore;                 // nullable: [chunk] records inside the chunk's own core (a contiguous run:
     int* first_in;              //   the walk only moves forward) and the index of the first of them
     int exact_only;             // 1: always the serial-recurrence preamble search (test hook, OFDM_WALK_EXACT=1)
-    // FFT correlation for the preamble search (cycles + L <= WALK_FFT_M): the
-    // template's spectrum and the M-point twiddles, or nullptr (direct search)
+    // FFT correlation for the preamble search (windows of WALK_FFT_M - L + 1
+    // lags, L <= WALK_FFT_M - 63): the template's spectrum and the M-point
+    // twiddles, or nullptr (direct search)
     const double2* tw_m;        // WALK_FFT_M forward twiddles
     const double2* tspec;       // sum_j c_j e^{+2 pi i k j / M}, k < M
     double tspec_max;           // max_k |tspec_k| (error bound)
 };
-constexpr int WALK_FFT_LOGM = 10;
+constexpr int WALK_FFT_LOGM = 9;
 constexpr int WALK_FFT_M = 1 << WALK_FFT_LOGM;
 
 struct GatherArgs {
