@@ -1170,7 +1170,8 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     // walkers: one chunk per resident walker slot (a single round: every
     // chunk re-walks a 3-frame halo to meet the true walk, so fewer, longer
     // chunks cost less), each >= 8 frames
-    const long slots = ofdm::stream_walk_slots();
+    const long slots = ofdm::stream_walk_slots(c->t2_logn, (int)c->p.pr_sin_len,
+                                               (int)(2 * c->p.t2sin_size + c->p.pr_sin_len), c->d_tspec != nullptr);
     // Knobs (environment, for experiments and tests): chunks per walker slot,
     // walk-in halo and walk-on extension in 1/1000 frames. Defaults: one
     // chunk per slot, 3-frame halo, no extension (tools/walk_q_sweep.sh:
@@ -1192,7 +1193,8 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     // samples) and the preamble window: this many records always suffice
     // (chunk 0 walks in from `start`, the others a halo before their core)
     const int max_rec =
-        (int)((chunk + std::max(halo, own_lo - start) + ext + 2048 + 2 * c->p.t2sin_size + c->p.pr_sin_len) / msg + 4);
+        (int)((chunk + std::max(halo, own_lo - start) + std::max(ext, 2 * flen) + 2048 + 2 * c->p.t2sin_size +
+               c->p.pr_sin_len) / msg + 4);
     int rc;
     const size_t rec_b = (size_t)nchunks * max_rec * sizeof(long);
     const size_t walk_b0 = rec_b + (size_t)nchunks * (sizeof(long) + sizeof(int)) + 2 * sizeof(long) + 64;
@@ -1237,6 +1239,12 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     w.core_lo = own_lo;
     w.core_hi = own_hi;
     w.ext = ext;
+    // A chunk whose core end falls inside a T2 scan (its last frame well
+    // before the end, e.g. a frame the reference's walk misses) walks on to
+    // the next frame it locates: the next chunk's walk locates that frame
+    // too, so the two sync without a serial re-walk (2048 chunks of config 4:
+    // one re-walk per call without this).
+    w.ext_scan = std::max(ext, 2 * flen);
     w.max_rec = max_rec;
     w.rec = d_rec;
     w.nrec = d_nrec;
@@ -1446,6 +1454,13 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
             for (long pb : lst)
                 if (pb <= first_owned && std::find(prev.begin(), prev.end(), pb) != prev.end()) sync = true;
             if (!sync) {
+                if (getenv("OFDM_STREAM_DEBUG")) {
+                    fprintf(stderr, "ofdm_rx_stream: re-walk chunk %ld [%ld, %ld) from %ld; its walk:", k, lo, hi, texit);
+                    for (long pb : lst) fprintf(stderr, " %ld", pb);
+                    fprintf(stderr, " | previous:");
+                    for (long pb : prev) fprintf(stderr, " %ld", pb);
+                    fprintf(stderr, "\n");
+                }
                 if ((rc = rewalk(k, texit))) return rc;
                 if (nrec[k] > max_rec) return fail(OFDM_ERR_HIP, "stream walk record overflow");
                 lst.assign(rec + (size_t)k * max_rec, rec + (size_t)k * max_rec + nrec[k]);

@@ -494,6 +494,37 @@ __device__ __forceinline__ void fft_regs_wave(double2 (&v)[8], int t, const doub
     fft_regs_tail_wave<LOGN, 1, SIGN>(v, t, lds_tw, lds);
 }
 
+// fft_block run by ONE wave (N = 512): natural-order result X[0..N) in lds
+// (index lds_swz(k)), visible to the wave on exit.
+template <int LOGN, int PASS, int SIGN>
+__device__ __forceinline__ void fft_tail_wave(double2 (&v)[8], int t, const double2* __restrict__ lds_tw,
+                                              double2* __restrict__ lds)
+{
+    using S = FftShape<LOGN>;
+    constexpr int NPASS = S::NPASS8 + (S::REM ? 1 : 0);
+    if constexpr (PASS < NPASS) {
+        constexpr bool is8 = PASS < S::NPASS8;
+        constexpr int R = is8 ? 8 : (1 << S::REM);
+        constexpr int NS = 1 << (3 * PASS);
+        const auto tw = pass_twiddles<LOGN, R, NS, SIGN>(t, lds_tw);
+        wave_lds_sync();  // previous pass fully written
+        lds_load8<LOGN>(v, t, lds);
+        wave_lds_sync();  // every lane has read before the image is overwritten
+        stockham_apply<LOGN, R, NS, SIGN>(v, t, tw, lds);
+        fft_tail_wave<LOGN, PASS + 1, SIGN>(v, t, lds_tw, lds);
+    }
+}
+
+template <int LOGN, int SIGN>
+__device__ __forceinline__ void fft_block_wave(double2 (&v)[8], int t, const double2* __restrict__ lds_tw,
+                                               double2* __restrict__ lds)
+{
+    static_assert(LOGN == 9, "one wave = N/8 = 64 threads");
+    stockham_pass<LOGN, 8, 1, SIGN>(v, t, lds_tw, lds);
+    fft_tail_wave<LOGN, 1, SIGN>(v, t, lds_tw, lds);
+    wave_lds_sync();
+}
+
 // ---------------------------------------------------------------- ping-pong
 // Same transform over two LDS images: pass p writes buf[(start + p) & 1] and
 // pass p+1 reads it, so one barrier per pass suffices (a buffer is only

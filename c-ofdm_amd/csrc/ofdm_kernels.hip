@@ -941,6 +941,190 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
     leave();
 }
 
+// ------------------------------------------------------------------ stream rx, two waves per frame
+// rx_kernel's stream mode (SYNC) for N = 512, where one transform is one
+// wave: the frame's message symbols are split over two waves, wave w
+// transforming s = w, w + 2, ..., so each wave holds half of the frame's
+// register window (RX_SMAX/2 symbols x RX_DPT carriers = 64 VGPRs) and the
+// kernel runs 3 waves per SIMD (155 VGPRs; rx_kernel: 2 at 256), 6 frames
+// per CU each transformed by two waves at once (LDS: one image per wave; the
+// transforms sync within their wave). No prefetch registers: the other waves
+// of the SIMD cover the load latency.
+// The arithmetic is rx_kernel's, operation for operation: the phase ramp,
+// the transform, phys (wave 0, the same lane order), the gains, the channel
+// reciprocal multiply (the fused stream decode's chan_recip mode; D <= 256),
+// the decisions.
+template <bool I16>
+__global__ void __launch_bounds__(128, 3) rx_stream2_kernel(RxArgs a)
+{
+    constexpr int LOGN = 9, N = 512, T = 64, SH = RX_SMAX / 2;
+    extern __shared__ double2 smem[];
+    const int S = a.S, D = a.D, P = a.P;
+    double2* lds_tw = smem + 2 * N;                          // TwLds::SIZE
+    double2* pil = lds_tw + TwLds<LOGN>::SIZE;               // S*P raw pilots
+    double2* gain = pil + S * P;                             // S*P equaliser gains
+    double* red = reinterpret_cast<double*>(gain + S * P);   // phys
+    uint8_t* dec = reinterpret_cast<uint8_t*>(smem);         // S*D decisions: the images, after the transforms
+    const int tid = threadIdx.x, lane0 = tid & 63;
+    const long nfr = a.count ? min(*a.count, a.nframes) : a.nframes;
+    if ((long)blockIdx.x >= nfr) return;  // uniform
+    load_twiddles<LOGN>(a.tab.tw, lds_tw, tid, 128);
+    int pk[RX_DPT];
+#pragma unroll
+    for (int i = 0; i < RX_DPT; ++i) pk[i] = a.tab.rx_pack[lane0 + T * i];
+    const int pbin = a.tab.pilot_swz[lane0];
+    const int m = 1 << (a.k / 2);
+    const double s1 = a.k == 1 ? 0.0 : 1.0 / (2.0 / (m - 1));
+    const long bpf = a.bytes_per_frame;
+    const bool by_word = (a.k == 1 || a.k == 2 || a.k == 4 || a.k == 8) && (bpf & 3) == 0 &&
+                         ((uintptr_t)a.bytes & 3) == 0;
+    const int L = N + a.cp;
+    __syncthreads();  // twiddles visible
+#pragma unroll 1
+    for (long f = blockIdx.x; f < nfr; f += gridDim.x) {
+        // opaque per-frame copies: addresses derived from them are recomputed
+        // per frame, not held live beside the register window
+        int lane;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(lane0));
+#pragma unroll
+        for (int i = 0; i < RX_DPT; ++i) asm volatile("" : "+v"(pk[i]));
+        const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+        double2* img = smem + w * N;
+        const long x0 = a.starts[f] + a.start_off;
+        double2 y[SH][RX_DPT];
+        // the wave's symbols, unrolled (compile-time window registers); each
+        // starts from an opaque lane copy and a memory fence, so nothing of one
+        // symbol (loads, LDS addresses) is hoisted and held across another
+#pragma unroll
+        for (int q = 0; q < SH; ++q) {
+            const int s = 2 * q + w;
+            if (s < S) {  // uniform
+                asm volatile("" ::: "memory");
+                int lq;
+                asm volatile("v_mov_b32 %0, %1" : "=v"(lq) : "v"(lane));
+                // the ramp's start phasor first (its sincos temporaries die
+                // before the sample registers are allocated)
+                const double* cr = a.corr + (f * S + s) * 4;
+                double sn, cs;
+                sincos(cr[0] + cr[1] * (double)lq, &sn, &cs);
+                double2 c = make_double2(cs, sn);
+                const double2 wr = make_double2(cr[2], cr[3]);
+                asm volatile("" ::: "memory");
+                double2 v[8];
+                const long off = x0 + (long)s * L + lq;
+                if constexpr (I16) {
+                    const int* p = reinterpret_cast<const int*>(a.iq16 + off);
+                    int r[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) r[i] = __builtin_nontemporal_load(p + T * i);
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+                        v[i] = make_double2((double)(int)(short)(r[i] & 0xffff), (double)(r[i] >> 16));
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) v[i] = load_nt(a.iq + off + T * i);
+                }
+                // sample m = lq + T*i of the body: *= e^{i(A + B m)}, by a
+                // running product from e^{i(A + B lq)} in steps of e^{i B T}
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    v[i] = cmul(v[i], c);
+                    if (i < 7) c = cmul(c, wr);
+                }
+                fft_block_wave<LOGN, -1>(v, lq, lds_tw, img);
+                if (lq < P) pil[s * P + lq] = img[pbin];
+#pragma unroll
+                for (int i = 0; i < RX_DPT; ++i) y[q][i] = img[pk[i] & 0xffff];
+                wave_lds_sync();  // read before the next transform rewrites the image
+            }
+        }
+        __syncthreads();  // both waves' pilots visible; the images are free
+        // the frame's channel reciprocals (main.cpp:69-71's divisors) to LDS,
+        // past the decisions in the free images; requested now, stored after
+        // the gains (the emit's stores would queue in front of loads issued there)
+        double2* chl = reinterpret_cast<double2*>(smem) + ((S * D + 15) >> 4);
+        const double2* chan = a.chan + f * a.chan_stride;
+        double2 chv[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {  // D <= 256 = 2 x 128
+            const int d = tid + 128 * u;
+            chv[u] = chan[d < D ? d : 0];
+        }
+        // phys_pilot_ampl = sum |pilot| / (P*S*pilot_ampl)   (Frame.cpp:76-80),
+        // summed by wave 0 in rx_kernel's lane order
+        if (w == 0) {
+            double acc = 0.0;
+            for (int i = lane; i < S * P; i += T) acc += hypot(pil[i].x, pil[i].y);
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+            if (lane == 0) red[0] = acc;
+        }
+        __syncthreads();
+        const double phys = red[0] / ((double)(P * S) * a.pilot_ampl);
+        // out = (F/phys) / ((F[s,p]/phys) / (F[0,p]/phys)) = F * gain[s][j]   (Frame.cpp:82-93)
+        for (int i = tid; i < S * P; i += 128) {
+            const int j = i % P;
+            const double2 c0 = make_double2(pil[j].x / phys, pil[j].y / phys);
+            const double2 cs = make_double2(pil[i].x / phys, pil[i].y / phys);
+            const double2 coef = cdiv_exact(cs, c0);
+            const double2 g = cdiv_exact(make_double2(1.0, 0.0), coef);
+            gain[i] = make_double2(g.x / phys, g.y / phys);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+            if (tid + 128 * u < D) chl[tid + 128 * u] = chv[u];
+        __syncthreads();
+        auto emit = [&](int s, const double2 (&yw)[RX_DPT]) {
+            double2* cbase = a.constell ? a.constell + (f * S + s) * D : nullptr;
+#pragma unroll
+            for (int i = 0; i < RX_DPT; ++i) {
+                int d = lane + T * i, gi = s * P + (pk[i] >> 16);
+                asm volatile("" : "+v"(d), "+v"(gi));  // opaque: not hoisted and held
+                if (d < D) {
+                    double2 o = cmul_exact(yw[i], gain[gi]);
+                    o = cmul_exact(o, chl[d]);  // chan_recip (host-checked)
+                    if (cbase) store_nt(cbase + d, o);
+                    dec[s * D + d] = (uint8_t)decide_select(o, a.k, s1, m);
+                }
+            }
+        };
+#pragma unroll
+        for (int q = 0; q < SH; ++q) {
+            const int s = 2 * q + w;
+            if (s < S) emit(s, y[q]);  // uniform
+        }
+        __syncthreads();  // decisions visible
+        if (a.bytes) {
+            if (by_word) {
+                const int per_word = 32 / a.k;  // decisions per output word
+                for (long wd = tid; wd < bpf / 4; wd += 128) {
+                    const uint8_t* dw = dec + wd * per_word;
+                    uint32_t word;
+                    switch (a.k) {
+                        case 1: word = pack_word<1>(dw); break;
+                        case 2: word = pack_word<2>(dw); break;
+                        case 4: word = pack_word<4>(dw); break;
+                        default: word = pack_word<8>(dw); break;
+                    }
+                    reinterpret_cast<uint32_t*>(a.bytes + f * bpf)[wd] = word;
+                }
+            } else {
+                for (long jb = tid; jb < bpf; jb += 128) {
+                    int byte = 0;
+                    for (int b = 0; b < 8; ++b) {
+                        const long bit = jb * 8 + b;
+                        const long g = bit / a.k;
+                        const int within = (int)(bit % a.k);
+                        byte = (byte << 1) | ((dec[g] >> (a.k - 1 - within)) & 1);
+                    }
+                    a.bytes[f * bpf + jb] = (uint8_t)byte;
+                }
+            }
+        }
+        __syncthreads();  // dec / pil / gain are rewritten by the next frame
+    }
+}
+
 // ------------------------------------------------------------------ demap / map
 // Modulation::demod on n points: one thread per output byte.
 __global__ void demap_kernel(double2* pts, long n, int k, uint8_t* bytes, long nbytes)
@@ -1133,6 +1317,27 @@ static hipError_t rx_launch_n(const RxArgs& a, hipStream_t st)
     return hipGetLastError();
 }
 
+template <bool I16>
+static hipError_t rx_stream2_launch(const RxArgs& a, hipStream_t st)
+{
+    const size_t shm = sizeof(double2) * (2 * 512 + TwLds<9>::SIZE + 2 * (size_t)a.S * a.P) + 2 * sizeof(double);
+    if (shm > 160 * 1024) return hipErrorInvalidValue;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)rx_stream2_kernel<I16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        attr = true;
+    }
+    if (a.nframes <= 0) return hipSuccess;
+    // persistent: 12 waves per CU (3 per SIMD: 155 VGPRs) = 6 workgroups, as far as LDS allows
+    long per_cu = (long)(160 * 1024) / (long)shm;
+    if (per_cu > 6) per_cu = 6;
+    const long cap = per_cu * num_cus();
+    const long grid = a.nframes < cap ? a.nframes : cap;
+    hipLaunchKernelGGL(rx_stream2_kernel<I16>, dim3((unsigned)grid), dim3(128), shm, st, a);
+    return hipGetLastError();
+}
+
 template <int LOGN>
 static hipError_t rx_dispatch(const RxArgs& a, hipStream_t st, bool* staged)
 {
@@ -1143,6 +1348,10 @@ static hipError_t rx_dispatch(const RxArgs& a, hipStream_t st, bool* staged)
     if (!fits && a.ystage == nullptr) return hipErrorInvalidValue;
     if (a.starts) {  // stream mode: register window only
         if (!fits || !a.corr) return hipErrorInvalidValue;
+#ifndef OFDM_RX_STREAM1  // timing experiment only: one wave per frame at N = 512
+        if (LOGN == 9 && a.chan && a.chan_recip)
+            return a.iq16 ? rx_stream2_launch<true>(a, st) : rx_stream2_launch<false>(a, st);
+#endif
         return a.iq16 ? rx_launch_n<LOGN, false, true, true>(a, st) : rx_launch_n<LOGN, false, false, true>(a, st);
     }
     if (a.iq16)

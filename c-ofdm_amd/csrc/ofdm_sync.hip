@@ -1052,7 +1052,16 @@ __device__ unsigned long long g_walk_sub[8192 * 8];  // sub-phase clocks per wal
 #define WPROF(...)
 #endif
 
-constexpr int WALK_THREADS = 256;
+// Walker workgroup: 128 threads (2 waves) for T2sin_size <= 1024, so that 8
+// walkers share a CU (~19 KB of LDS each, 128 VGPRs = 4 waves per SIMD): the
+// walk is latency-bound, and twice the walkers halve each one's chunk. One
+// 256-thread transform for T2sin_size = 2048.
+template <int LOGT>
+struct WalkShape {
+    static constexpr int T = (1 << LOGT) / 8;
+    static constexpr int WT = T > 128 ? T : 128;  // threads
+    static constexpr int G = WT / T;              // T2 blocks per scan step
+};
 
 // Stream sample j as complex<double> (int16 wire samples convert exactly, as
 // FRAME_FORM::form_int16_to_double, Frame.hpp:472-481); zero outside [0, n).
@@ -1136,35 +1145,34 @@ __device__ __forceinline__ void load8_block(const A& a, long base, bool live, do
     }
 }
 
+__device__ __forceinline__ double energy_rn(double2 v) { return add_rn(mul_rn(v.x, v.x), mul_rn(v.y, v.y)); }
+
 // PREAMBLE_FORM::find_preamble from s: first lag with norm > 1 and
 // |sum_j x[s+i+j] c_j| / sqrt(norm) > level (Frame.cpp:338-378), INT_MAX if
 // none. Exact form: the running energy is the reference's serial recurrence
-// (+ new, then - old, separately rounded) on per-sample energies computed in
-// parallel; lags are tested 256 at a time with an early exit. xs: C + L
-// samples, E: C + L energies, normv: C running energies (all LDS).
-__device__ int walk_preamble_exact(const WalkArgs& a, long s, double2* xs, const double2* c, double* E,
-                                   double* normv, int* best, int t)
+// (+ new, then - old, separately rounded; each sample's energy as re*re+im*im
+// rounded as the reference rounds it); lags are tested WT at a time with an
+// early exit. xs: C + L samples, normv: C running energies (LDS).
+template <int WT>
+__device__ int walk_preamble_exact(const WalkArgs& a, long s, double2* xs, const double2* c, double* normv,
+                                   int* best, int t)
 {
     const int L = a.L, C = a.cycles;
-    for (int i = t; i < C + L; i += WALK_THREADS) {
-        const double2 v = stream_sample(a, s + i);
-        xs[i] = v;
-        E[i] = add_rn(mul_rn(v.x, v.x), mul_rn(v.y, v.y));
-    }
+    for (int i = t; i < C + L; i += WT) xs[i] = stream_sample(a, s + i);
     if (t == 0) *best = INT_MAX;
     __syncthreads();
     if (t == 0) {
         double norm = 0.0;
-        for (int i = 0; i < L; ++i) norm = add_rn(norm, E[i]);
+        for (int i = 0; i < L; ++i) norm = add_rn(norm, energy_rn(xs[i]));
         for (int i = 0; i < C; ++i) {
             normv[i] = norm;
-            norm = add_rn(norm, E[i + L]);
-            norm = sub_rn(norm, E[i]);
+            norm = add_rn(norm, energy_rn(xs[i + L]));
+            norm = sub_rn(norm, energy_rn(xs[i]));
         }
     }
     __syncthreads();
     int found = INT_MAX;
-    for (int base = 0; base < C; base += WALK_THREADS) {
+    for (int base = 0; base < C; base += WT) {
         const int i = base + t;
         if (i < C) {
             const double norm = normv[i];
@@ -1192,14 +1200,18 @@ __device__ int walk_preamble_exact(const WalkArgs& a, long s, double2* xs, const
 // than that bound is decided exactly as the reference decides it. The first
 // lag that is not a certain FAIL is the answer when it is a certain PASS;
 // otherwise (margins ~1e-13, practically never) the exact serial search runs.
-__device__ int walk_preamble(const WalkArgs& a, long s, double2* xs, const double2* c, double* E, double* normv,
+// xs: C + L samples, E: C + L energies, normv: C, c: the L template taps
+// (all in the search scratch; c is loaded here).
+template <int WT>
+__device__ int walk_preamble(const WalkArgs& a, long s, double2* xs, double2* c, double* E, double* normv,
                              int* best, int* unsure, double* mred, int t)
 {
     constexpr double U = 0x1.0p-53;
     const int L = a.L, C = a.cycles;
-    if (a.exact_only) return walk_preamble_exact(a, s, xs, c, E, normv, best, t);
+    if (a.exact_only) return walk_preamble_exact<WT>(a, s, xs, a.templ, normv, best, t);
+    for (int i = t; i < L; i += WT) c[i] = a.templ[i];
     double emax = 0.0;
-    for (int i = t; i < C + L; i += WALK_THREADS) {
+    for (int i = t; i < C + L; i += WT) {
         const double2 v = stream_sample(a, s + i);
         xs[i] = v;
         const double e2 = add_rn(mul_rn(v.x, v.x), mul_rn(v.y, v.y));
@@ -1212,13 +1224,13 @@ __device__ int walk_preamble(const WalkArgs& a, long s, double2* xs, const doubl
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) emax = fmax(emax, __shfl_xor(emax, o));
-    if ((t & 63) == 0) mred[WALK_THREADS / 64 + (t >> 6)] = emax;
+    if ((t & 63) == 0) mred[WT / 64 + (t >> 6)] = emax;
     double M = 0.0;  // max window sum over every lag so far
     int found = INT_MAX;
-    for (int base = 0; base < C; base += 2 * WALK_THREADS) {
+    for (int base = 0; base < C; base += 2 * WT) {
         __syncthreads();  // xs/E visible (first batch); best/unsure reset
         // two lags per thread, interleaved (two independent accumulation chains)
-        const int i0 = base + t, i1 = base + WALK_THREADS + t;
+        const int i0 = base + t, i1 = base + WT + t;
         const bool v0 = i0 < C, v1 = i1 < C;
         const int j0 = v0 ? i0 : 0, j1 = v1 ? i1 : 0;
         double2 e0 = make_double2(0.0, 0.0), e1 = make_double2(0.0, 0.0);
@@ -1236,10 +1248,10 @@ __device__ int walk_preamble(const WalkArgs& a, long s, double2* xs, const doubl
         for (int o = 32; o > 0; o >>= 1) mloc = fmax(mloc, __shfl_xor(mloc, o));
         if ((t & 63) == 0) mred[t >> 6] = mloc;
         __syncthreads();
-        double mb = mred[0], eb = mred[WALK_THREADS / 64];
-        for (int w = 1; w < WALK_THREADS / 64; ++w) {
+        double mb = mred[0], eb = mred[WT / 64];
+        for (int w = 1; w < WT / 64; ++w) {
             mb = fmax(mb, mred[w]);
-            eb = fmax(eb, mred[WALK_THREADS / 64 + w]);
+            eb = fmax(eb, mred[WT / 64 + w]);
         }
         M = fmax(M, mb);
         const double Mall = M + eb;  // bounds every partial value of the recurrence
@@ -1269,7 +1281,7 @@ __device__ int walk_preamble(const WalkArgs& a, long s, double2* xs, const doubl
         const int un = *unsure;
         if (found != INT_MAX) {  // uniform
             __syncthreads();     // every thread has read best/unsure
-            if (un == found) return walk_preamble_exact(a, s, xs, c, E, normv, best, t);
+            if (un == found) return walk_preamble_exact<WT>(a, s, xs, c, normv, best, t);
             return found;
         }
     }
@@ -1294,8 +1306,9 @@ __device__ int walk_preamble(const WalkArgs& a, long s, double2* xs, const doubl
 // certain FAIL must be a certain PASS, else the exact search runs. The other
 // waves wait at the closing barrier (the transforms synchronise within the
 // wave only). buf: M entries, P: M doubles (both in the search scratch).
+template <int WT>
 __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double* P, const double2* tw_m, int* res,
-                                 double2* xs, double* E, double* normv, int* best, int t)
+                                 double2* xs, double* normv, int* best, int t)
 {
     constexpr double U = 0x1.0p-53;
     constexpr int LM = WALK_FFT_LOGM, M = WALK_FFT_M, R = M / 64;
@@ -1431,27 +1444,45 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
     if (found < -1) {  // uniform: a lag within the error bounds of a threshold
         WPROF(if (t == 0) atomicAdd(&g_walk_fallbacks, 1ULL));
         lds_barrier();  // every wave has read *res (the exact search reuses the scratch)
-        return walk_preamble_exact(a, s, xs, a.templ, E, normv, best, t);
+        return walk_preamble_exact<WT>(a, s, xs, a.templ, normv, best, t);
     }
     return found;
 }
 
 }  // namespace
 
+// LDS of a walker: the fixed part, then the scratch (`big`) that the T2
+// transforms and the preamble searches share (they run one after the other).
 template <int LOGT>
-__global__ void __launch_bounds__(WALK_THREADS, 4) stream_walk_kernel(WalkArgs a)
+struct WalkLds {
+    static constexpr int WT = WalkShape<LOGT>::WT, G = WalkShape<LOGT>::G, T = WalkShape<LOGT>::T;
+    static constexpr int NW = T >= 64 ? T / 64 : 1;
+    static constexpr size_t FIXED = sizeof(double2) * (TwLds<LOGT>::SIZE + G * NW) + sizeof(double) * 2 * (WT / 64) +
+                                    16 + sizeof(double) * 16 + sizeof(double2) * TwLds<WALK_FFT_LOGM>::SIZE;
+    // scratch bytes: T2 images; FFT search (M samples + M prefix energies); exact
+    // search (C + L samples + C energies); direct search (+ C + L energies + L taps)
+    static size_t big(int L, int C, bool fft)
+    {
+        const size_t t2 = sizeof(double2) * (size_t)G * (1 << LOGT);
+        const size_t fs = fft ? (sizeof(double2) + sizeof(double)) * WALK_FFT_M : 0;
+        const size_t ex = sizeof(double2) * (size_t)(C + L) + sizeof(double) * C;
+        const size_t di = fft ? 0 : ex + sizeof(double) * (C + L) + 16 + sizeof(double2) * L;
+        return std::max(std::max(t2, fs), std::max(ex, di));
+    }
+};
+
+template <int LOGT>
+__global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(WalkArgs a)
 {
-    constexpr int N = 1 << LOGT, T = N / 8, G = WALK_THREADS / T;
-    static_assert(T <= WALK_THREADS, "T2sin_size <= 2048");
+    constexpr int N = 1 << LOGT, T = N / 8, WT = WalkShape<LOGT>::WT, G = WalkShape<LOGT>::G;
     constexpr int NW = T >= 64 ? T / 64 : 1;  // waves per transform
     // LDS: the T2 transforms and the preamble search run one after the other,
     // so their buffers alias (walk_lds_big): 4 walkers fit a CU
     extern __shared__ double2 smem[];
     double2* lds_tw = smem;
     double2* red = lds_tw + TwLds<LOGT>::SIZE;          // G * NW (tot, sine)
-    double2* ctap = red + G * NW;                       // L template taps
-    double* mred = reinterpret_cast<double*>(ctap + a.L);  // 2 * WALK_THREADS/64 maxima
-    int* best = reinterpret_cast<int*>(mred + 2 * (WALK_THREADS / 64));
+    double* mred = reinterpret_cast<double*>(red + G * NW);  // 2 * WT/64 maxima
+    int* best = reinterpret_cast<int*>(mred + 2 * (WT / 64));
     int* bestg = best + 1;
     int* unsure = best + 2;
     double* scr = reinterpret_cast<double*>(best + 4);  // 16 scan / max scratch
@@ -1462,16 +1493,16 @@ __global__ void __launch_bounds__(WALK_THREADS, 4) stream_walk_kernel(WalkArgs a
     double2* tw_m = reinterpret_cast<double2*>(scr + 16);  // TwLds<WALK_FFT_LOGM> (FFT search)
     double2* big = tw_m + TwLds<WALK_FFT_LOGM>::SIZE;
     double2* fftb = big;                                // G * N (T2 transforms)
-    double2* xs = big;                                  // cycles + L samples (preamble search)
-    double* E = reinterpret_cast<double*>(xs + a.cycles + a.L);  // cycles + L energies
-    double* normv = E + a.cycles + a.L;                 // cycles running energies (exact fallback)
+    double2* xs = big;                                  // cycles + L samples (exact / direct search)
+    double* normv = reinterpret_cast<double*>(xs + a.cycles + a.L);  // cycles running energies
+    double* E = normv + a.cycles;                       // cycles + L energies (direct search)
+    double2* ctap = reinterpret_cast<double2*>(reinterpret_cast<uintptr_t>(E + a.cycles + a.L + 1) & ~(uintptr_t)15);
     double* P = reinterpret_cast<double*>(big + WALK_FFT_M);  // a window's prefix energies (FFT search)
 
     int* qslot = best + 3;  // the chunk taken from the queue
     const int t0 = threadIdx.x;
-    load_twiddles<LOGT>(a.t2tw, lds_tw, t0, WALK_THREADS);
-    if (a.tspec) load_twiddles<WALK_FFT_LOGM>(a.tw_m, tw_m, t0, WALK_THREADS);
-    for (int i = t0; i < a.L; i += WALK_THREADS) ctap[i] = a.templ[i];
+    load_twiddles<LOGT>(a.t2tw, lds_tw, t0, WT);
+    if (a.tspec) load_twiddles<WALK_FFT_LOGM>(a.tw_m, tw_m, t0, WT);
     if (t0 == 0) {
         *bestg = INT_MAX;
         bslot[0] = INT_MAX;
@@ -1532,7 +1563,10 @@ __global__ void __launch_bounds__(WALK_THREADS, 4) stream_walk_kernel(WalkArgs a
             }
             if (base >= end) {  // scanning past the core: an equivalent state
                 if (exitp < 0) exitp = base;
-                if (base >= end + a.ext) {
+                // the end fell inside a scan: walk on to the next located frame
+                // (within ext_scan), so that the next chunk's walk, which
+                // locates it too, syncs with this one without a re-walk
+                if (base >= end + a.ext_scan) {
                     stop = true;
                     break;
                 }
@@ -1599,9 +1633,9 @@ __global__ void __launch_bounds__(WALK_THREADS, 4) stream_walk_kernel(WalkArgs a
         if (stop) break;
         WPROF(++p_np;)
         const int lag = (a.tspec && !a.exact_only)
-                            ? walk_preamble_fft(a, hit, big, P, tw_m, reinterpret_cast<int*>(scr + 2), xs, E, normv,
-                                                best, t)
-                            : walk_preamble(a, hit, xs, ctap, E, normv, best, unsure, mred, t);
+                            ? walk_preamble_fft<WT>(a, hit, big, P, tw_m, reinterpret_cast<int*>(scr + 2), xs, normv,
+                                                    best, t)
+                            : walk_preamble<WT>(a, hit, xs, ctap, E, normv, best, unsure, mred, t);
         WPROF(p_pre += clock64() - p_b;)
         const long pb = (lag == INT_MAX ? -10 : hit + lag) + 1;  // rx.cpp:160
         if (pb < -2) {                                            // rx.cpp:162-168
@@ -1649,14 +1683,15 @@ __global__ void gather_kernel(GatherArgs a)
 }
 
 template <int LOGT>
+static size_t walk_shm(int L, int C, bool fft)
+{
+    return WalkLds<LOGT>::FIXED + WalkLds<LOGT>::big(L, C, fft);
+}
+
+template <int LOGT>
 static hipError_t walk_launch_n(const WalkArgs& a, long nblocks, hipStream_t st)
 {
-    constexpr int N = 1 << LOGT, T = N / 8, G = WALK_THREADS / T, NW = T >= 64 ? T / 64 : 1;
-    const size_t search = sizeof(double2) * ((size_t)a.cycles + a.L) + sizeof(double) * (2 * (size_t)a.cycles + a.L);
-    const size_t fsearch = a.tspec ? (sizeof(double2) + sizeof(double)) * WALK_FFT_M : 0;
-    const size_t big = std::max(std::max(sizeof(double2) * (size_t)G * N, search), fsearch);
-    const size_t shm = sizeof(double2) * (TwLds<LOGT>::SIZE + G * NW + a.L) + sizeof(double) * 2 * (WALK_THREADS / 64) +
-                       16 + sizeof(double) * 16 + sizeof(double2) * TwLds<WALK_FFT_LOGM>::SIZE + big;
+    const size_t shm = walk_shm<LOGT>(a.L, a.cycles, a.tspec != nullptr);
     if (shm > 160 * 1024) return hipErrorInvalidValue;
     static bool attr = false;
     if (!attr) {
@@ -1664,21 +1699,43 @@ static hipError_t walk_launch_n(const WalkArgs& a, long nblocks, hipStream_t st)
                                   160 * 1024);
         attr = true;
     }
-    hipLaunchKernelGGL(stream_walk_kernel<LOGT>, dim3((unsigned)nblocks), dim3(WALK_THREADS), shm, st, a);
+    hipLaunchKernelGGL(stream_walk_kernel<LOGT>, dim3((unsigned)nblocks), dim3(WalkShape<LOGT>::WT), shm, st, a);
     return hipGetLastError();
 }
 
-long stream_walk_slots()
+template <int LOGT>
+static long walk_slots_n(int L, int C, bool fft)
 {
-    static long cache[64] = {0};
-    int dev = 0;
+    int dev = 0, ncu = 0, per = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-    if (!cache[dev]) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-        cache[dev] = 4L * n;  // __launch_bounds__(WALK_THREADS, 4): 4 walkers per CU
+    static long cache[64][4] = {};  // device: {L, C, fft, slots} of the last query
+    long* q = cache[dev];
+    if (q[3] && q[0] == L && q[1] == C && q[2] == (long)fft) return q[3];
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+    (void)hipFuncSetAttribute((const void*)stream_walk_kernel<LOGT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)stream_walk_kernel<LOGT>, WalkShape<LOGT>::WT,
+                                                     walk_shm<LOGT>(L, C, fft)) != hipSuccess ||
+        per <= 0)
+        per = 1;
+    q[0] = L;
+    q[1] = C;
+    q[2] = fft;
+    q[3] = (long)per * ncu;
+    return q[3];
+}
+
+long stream_walk_slots(int logt, int L, int C, bool fft)
+{
+    switch (logt) {
+        case 6: return walk_slots_n<6>(L, C, fft);
+        case 7: return walk_slots_n<7>(L, C, fft);
+        case 8: return walk_slots_n<8>(L, C, fft);
+        case 9: return walk_slots_n<9>(L, C, fft);
+        case 10: return walk_slots_n<10>(L, C, fft);
+        case 11: return walk_slots_n<11>(L, C, fft);
+        default: return 256;
     }
-    return cache[dev];
 }
 
 hipError_t launch_stream_walk(int logt, const WalkArgs& a, long nblocks, hipStream_t st)

@@ -89,6 +89,7 @@ struct WalkArgs {
     long start;                 // walk state chunk 0 starts from (0: the stream's first sample)
     long core_lo, core_hi;      // the chunk cores tile [core_lo, core_hi) (whole stream: [0, n))
     long ext;                   // walk-on past the core end while looking for the first frame there
+    long ext_scan;              // >= ext: the same when the core end falls inside a T2 scan
     const int* chunk_ids;       // nullable: chunk of each workgroup (re-walk launches)
     const long* start_pos;      // nullable: exact start state per workgroup (re-walk)
     int* queue;                 // nullable: chunk counter (zeroed) the workgroups take chunks from until
@@ -162,8 +163,9 @@ hipError_t launch_compact(const CompactArgs& a, hipStream_t st);
 hipError_t launch_stream_params(int logn, const StreamParamsArgs& a, hipStream_t st);
 
 hipError_t launch_stream_walk(int logt, const WalkArgs& a, long nblocks, hipStream_t st);
-// stream walkers resident at once on the current device (4 per CU)
-long stream_walk_slots();
+// stream walkers resident at once on the current device (occupancy of the
+// walker with this geometry's LDS: 8 per CU for the default geometries)
+long stream_walk_slots(int logt, int L, int C, bool fft);
 hipError_t launch_gather(const GatherArgs& a, hipStream_t st);
 hipError_t launch_t2_scan(int logn, const T2Args& a, int* first_out, hipStream_t st);
 hipError_t launch_find_preamble(const PreambleArgs& a, hipStream_t st);
