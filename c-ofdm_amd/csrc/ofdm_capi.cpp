@@ -1303,8 +1303,6 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
             ca.P = c->P;
             ca.cfo_out = cfo;
             ca.count = d_cnt;  // single batch when set (f0 == 0)
-            hipError_t e2 = ofdm::launch_cfo(pl->logm, pl->g, ca, st);
-            if (e2 != hipSuccess) return hip_fail(e2, "stream cfo launch");
             ofdm::StreamParamsArgs sa{};
             sa.tab = c->tables(true);
             sa.iq = reinterpret_cast<const double2*>(iq);
@@ -1324,8 +1322,20 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
             sa.cp = c->cp;
             sa.pilot_ampl = (double)c->p.pilot_ampl / 1000;
             sa.count = d_cnt;
-            e2 = ofdm::launch_stream_params(c->logn, sa, st);
-            if (e2 != hipSuccess) return hip_fail(e2, "stream params launch");
+            // one kernel for pilot_freq_sinh + the params stage where the
+            // geometry allows (N = 512, 640-point CFO form), else two
+            hipError_t e2 = hipErrorNotSupported;
+#ifndef OFDM_STREAM_SYNC2  // timing experiment only: the two-kernel path
+            e2 = ofdm::launch_stream_sync(ca, sa, c->logn, pl->logm, pl->g, st);
+#endif
+            if (e2 == hipErrorNotSupported) {
+                e2 = ofdm::launch_cfo(pl->logm, pl->g, ca, st);
+                if (e2 != hipSuccess) return hip_fail(e2, "stream cfo launch");
+                e2 = ofdm::launch_stream_params(c->logn, sa, st);
+                if (e2 != hipSuccess) return hip_fail(e2, "stream params launch");
+            } else if (e2 != hipSuccess) {
+                return hip_fail(e2, "stream sync launch");
+            }
             ofdm::RxArgs ra{};
             ra.tab = c->tables(false);
             ra.iq = reinterpret_cast<const double2*>(iq);

@@ -494,8 +494,8 @@ __device__ __forceinline__ void fft_regs_wave(double2 (&v)[8], int t, const doub
     fft_regs_tail_wave<LOGN, 1, SIGN>(v, t, lds_tw, lds);
 }
 
-// fft_block run by ONE wave (N = 512): natural-order result X[0..N) in lds
-// (index lds_swz(k)), visible to the wave on exit.
+// fft_block run within ONE wave (N <= 512): natural-order result X[0..N) in
+// lds (index lds_swz(k)), visible to the wave on exit.
 template <int LOGN, int PASS, int SIGN>
 __device__ __forceinline__ void fft_tail_wave(double2 (&v)[8], int t, const double2* __restrict__ lds_tw,
                                               double2* __restrict__ lds)
@@ -515,11 +515,13 @@ __device__ __forceinline__ void fft_tail_wave(double2 (&v)[8], int t, const doub
     }
 }
 
+// For N < 512 a wave holds 512/N transforms side by side (t: the thread's
+// index within its transform, lds: that transform's image).
 template <int LOGN, int SIGN>
 __device__ __forceinline__ void fft_block_wave(double2 (&v)[8], int t, const double2* __restrict__ lds_tw,
                                                double2* __restrict__ lds)
 {
-    static_assert(LOGN == 9, "one wave = N/8 = 64 threads");
+    static_assert(LOGN >= 6 && LOGN <= 9, "N/8 <= one wave");
     stockham_pass<LOGN, 8, 1, SIGN>(v, t, lds_tw, lds);
     fft_tail_wave<LOGN, 1, SIGN>(v, t, lds_tw, lds);
     wave_lds_sync();

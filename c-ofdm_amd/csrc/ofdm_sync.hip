@@ -100,9 +100,10 @@ __device__ __forceinline__ unsigned umap_then(unsigned f, unsigned g)  // f, the
 // ph[0..n) raw phases in LDS (visible to every thread); on return they are
 // unwrapped and visible. All NT threads call it; scr: NT/64 words of LDS.
 // n - 1 <= 4 * NT (chan_char_lq: n = D/2 <= N/2 = 4 * NT).
-template <int NT>
+template <int NT, bool WAVE = false>
 __device__ void unwrap_scan(double* ph, int n, unsigned* scr)
 {
+    static_assert(!WAVE || NT == 64, "a wave-local scan is one wave");
     const int t = threadIdx.x, lane = t & 63;
     const int R = (n - 1 + NT - 1) / NT;  // entries 1..n-1, R consecutive per thread
     const int i0 = 1 + t * R;
@@ -144,7 +145,10 @@ __device__ void unwrap_scan(double* ph, int n, unsigned* scr)
         for (int w = 0; w < (t >> 6); ++w) pre = umap_then(pre, scr[w]);
         ex = umap_then(pre, ex);
     }
-    __syncthreads();  // every raw phase has been read
+    if constexpr (WAVE)
+        wave_lds_sync();
+    else
+        __syncthreads();  // every raw phase has been read
     int st = (ex >> 2) & 3;  // entry 0 is never adjusted (state 1)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -154,7 +158,10 @@ __device__ void unwrap_scan(double* ph, int n, unsigned* scr)
             ph[i] = st == 1 ? raw[r] : (st == 0 ? raw[r] - 2 * M_PI : raw[r] + 2 * M_PI);
         }
     }
-    __syncthreads();
+    if constexpr (WAVE)
+        wave_lds_sync();
+    else
+        __syncthreads();
 }
 
 }  // namespace
@@ -1026,6 +1033,354 @@ hipError_t launch_stream_params(int logn, const StreamParamsArgs& a, hipStream_t
         case 12: return params_launch_n<12>(a, st);
         default: return hipErrorInvalidValue;
     }
+}
+
+// ========================================================================
+// Fused stream decode, stages 1 + 2 in one kernel, for N = 512 and a
+// pilot_freq_sinh form of 640 = 5 x 128 points (the D geometry): two waves
+// per located frame, the preamble read once for both stages.
+//   wave 0: pilot_freq_sinh as cfo_kernel<7, 5> (five interleaved 128-point
+//           transforms, four side by side and then one, the radix-5 combine,
+//           |.|, fftshift, first argmax per window), then the preamble part
+//           of stream_params_kernel (its cp_freq_sinh phase, freq_shift +
+//           cp correction, the body FFT, pr_phase_sinh, chan_char_lq);
+//   wave 1: meanwhile the message symbols' CP correlation sums (raw samples;
+//           rotated once the CFO is known).
+// Then both waves: the symbol phases, the channel reciprocals and the ramps.
+// Every quantity is computed with the arithmetic of the two kernels it
+// replaces (same transforms, same reduction orders), so the results are the
+// same to the last bit.
+// ========================================================================
+__global__ void __launch_bounds__(128, 4) stream_sync_kernel(CfoArgs c, StreamParamsArgs a)
+{
+    // the geometry is fixed (host-checked): N = 512, cp = 128, L = 640 = 10 T
+    constexpr int LOGN = 9, N = 512, T = 64, LOGM = 7, M = 128, G = 5, S5 = G * M, CP = 128, L = N + CP;
+    constexpr int LT = L / T, CT = CP / T, RMAX = LT;
+    extern __shared__ double2 smem[];
+    double2* tw9 = smem;                                    // TwLds<9>
+    double2* tw7 = tw9 + TwLds<LOGN>::SIZE;                 // TwLds<7>
+    double2* img = tw7 + TwLds<LOGM>::SIZE;                 // G * M: the CFO transforms, then the body FFT
+    double2* pil = img + S5;                                // P
+    double2* dat = pil + a.P;                               // D/2 raw bins of the preamble
+    double2* red = dat + (a.D / 2 + 1);                     // 32
+    double2* cps = red + 32;                                // 1 + S raw CP sums
+    double* amp = reinterpret_cast<double*>(img);           // S5 magnitudes (fftshifted), over the transforms
+    double* ph = reinterpret_cast<double*>(cps + 1 + a.S);  // D/2 + 2
+    double* phi = ph + a.D / 2 + 2;                         // 64 symbol phases
+    double* psi = phi + 64;                                 // 64 prefix sums
+    double* scal = psi + 64;                                // cfo, phr, b, aa
+    int* wsum = reinterpret_cast<int*>(scal + 4);           // P + 1 window maxima
+    const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const long f = blockIdx.x;
+    if (a.count && f >= *a.count) return;  // uniform: past the speculative frame count
+    const long x0 = a.starts[f];
+    const int half = a.D / 2, Q = 1 + a.S;
+    // ---------------------------------------------------------- pilot_freq_sinh (both waves)
+    // transform g holds x[G*n + g], n = tt + 16*i: g = lane/16 (0..3) on
+    // wave 0, g = 4 on wave 1's lanes 0..15
+    {
+        const int g = w == 0 ? lane >> 4 : 4, tt = lane & 15;
+        double2 v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const long j = x0 + (long)G * (tt + 16 * i) + g;
+            if (c.x16) {
+                const short2 q0 = c.x16[j];
+                v[i] = make_double2((double)q0.x, (double)q0.y);
+            } else {
+                v[i] = c.x[j];
+            }
+        }
+        load_twiddles<LOGM>(c.tw_sub, tw7, tid, 128);
+        load_twiddles<LOGN>(a.tab.tw, tw9, tid, 128);
+        __syncthreads();  // twiddles visible
+        if (w == 0 || lane < 16) fft_block_wave<LOGM, -1>(v, tt, tw7, img + g * M);
+        __syncthreads();  // the five transforms visible
+    }
+    {
+        // X[k + M*r] = sum_q W_S^{q k} W_G^{q r} F_q[k]; amp stored fftshifted:
+        // shifted[i] = spec[(i + S/2) % S]  (Frame.hpp:300-305)
+        constexpr int half5 = S5 / 2;
+        double2 twg[G - 1];
+#pragma unroll
+        for (int q = 1; q < G; ++q) twg[q - 1] = c.tw_full[(long)q * M];
+        {
+            const int k = tid;  // M = 128 = the workgroup
+            double2 twk[G - 1];
+#pragma unroll
+            for (int q = 1; q < G; ++q) twk[q - 1] = c.tw_full[(long)q * k % S5];
+            double2 tq[G];
+#pragma unroll
+            for (int q = 0; q < G; ++q) {
+                const double2 fq = img[q * M + lds_swz(k)];
+                tq[q] = q == 0 ? fq : cmul(fq, twk[q - 1]);
+            }
+            __syncthreads();  // every transform read: amp overwrites them
+#pragma unroll
+            for (int r = 0; r < G; ++r) {
+                double2 acc = tq[0];
+#pragma unroll
+                for (int q = 1; q < G; ++q)
+                    acc = cadd(acc, cmul(tq[q], (q * r) % G ? twg[(q * r) % G - 1] : make_double2(1.0, 0.0)));
+                const int idx = k + M * r;
+                amp[(idx + half5) % S5] = hypot(acc.x, acc.y);
+            }
+        }
+        __syncthreads();  // amp visible
+        // first argmax inside each pilot window [borders[i], borders[i+1]), i != P/2
+        // (std::max_element: 8-lane groups, the larger value, the lower index on ties)
+        constexpr int AG = 8;
+        for (int i0 = 0; i0 <= c.P; i0 += 128 / AG) {
+            const int i = i0 + tid / AG, l = tid % AG;
+            const bool act = i <= c.P;
+            int lo = 0, hi = 0;
+            if (act) {
+                lo = c.borders[i];
+                hi = c.borders[i + 1];
+            }
+            double bv = -1.0;
+            int bi = INT_MAX;
+            for (int j = lo + l; j < hi; j += AG)
+                if (bv < amp[j]) {
+                    bv = amp[j];
+                    bi = j;
+                }
+#pragma unroll
+            for (int o = 1; o < AG; o <<= 1) {
+                const double ov = __shfl_xor(bv, o);
+                const int oi = __shfl_xor(bi, o);
+                if (ov > bv || (ov == bv && oi < bi)) {
+                    bv = ov;
+                    bi = oi;
+                }
+            }
+            if (act && l == 0) wsum[i] = lo < hi ? (isnan(amp[lo]) ? lo : bi) : hi;
+        }
+        __syncthreads();  // window maxima visible
+        if (tid == 0) {
+            double shift = 0.0;
+            for (int i = 0; i <= c.P; ++i)
+                if (i != c.P / 2) shift += wsum[i];
+            shift /= c.P;
+            shift -= S5 / 2;
+            shift /= S5;
+            scal[0] = shift;
+            c.cfo_out[f] = shift;
+        }
+        __syncthreads();  // the CFO visible; the CFO images are free
+    }
+    if (w == 0) {
+        const double cfo = scal[0];
+
+        // ---------------------------------------------------------- preamble (stream_params_kernel)
+        const int t = lane;
+        int dbin[4], dslot[2];
+        double2 mpre[4], prc[2];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = t + T * u;
+            dbin[u] = i < a.D ? a.tab.data_bin[i] : 0;
+            mpre[u] = i < a.D ? a.mod_pre[i] : make_double2(0.0, 0.0);
+            if (u < 2) {
+                dslot[u] = i < half ? a.tab.data_slot[i] : 0;
+                prc[u] = u < CT ? a.pre[i] : make_double2(0.0, 0.0);
+            }
+        }
+        const int pbin = t < a.P ? a.tab.pilot_bin[t] : 0;
+        double2 z[RMAX];
+#pragma unroll
+        for (int r = 0; r < RMAX; ++r)
+            z[r] = r < LT ? src_sample(a.iq, a.iq16, x0 + t + (long)T * r) : make_double2(0.0, 0.0);
+        double rs, rc;
+        sincospi(-2.0 * cfo * (double)N, &rs, &rc);
+        {
+            // the preamble's cp_freq_sinh sum (CP sample r pairs with r + N/T)
+            double2 acc = make_double2(0.0, 0.0);
+#pragma unroll
+            for (int r = 0; r < RMAX; ++r)
+                if (r < CT && r + N / T < RMAX) acc = cadd(acc, cconj_mul(z[r], z[r + N / T]));
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                acc.x += __shfl_xor(acc.x, o);
+                acc.y += __shfl_xor(acc.y, o);
+            }
+            acc = cadd(make_double2(0.0, 0.0), acc);
+            const double2 rr = cmul_exact(acc, make_double2(rc, rs));
+            if (t == 0) phi[0] = atan2(rr.y, rr.x);
+        }
+        wave_lds_sync();
+        const double slope0 = -2.0 * M_PI * cfo - phi[0] / N;
+        double phr;
+        {
+            double sn, cs, ws, wc;
+            sincos(slope0 * (double)t, &sn, &cs);
+            sincos(slope0 * (double)T, &ws, &wc);
+            double2 cc = make_double2(cs, sn);
+            const double2 wv = make_double2(wc, ws);
+            double2 acc = make_double2(0.0, 0.0);
+#pragma unroll
+            for (int r = 0; r < RMAX; ++r) {
+                if (r < LT) {
+                    z[r] = cmul_exact(z[r], cc);
+                    if (r < 2 && r < CT) acc = cadd(acc, cconj_mul(prc[r], z[r]));
+                    cc = cmul(cc, wv);
+                }
+            }
+            double2* fftb = img;  // the CFO images are free
+#pragma unroll
+            for (int r = 0; r < RMAX; ++r)
+                if (r >= CT && r < LT) fftb[(r - CT) * T + t] = z[r];
+            wave_lds_sync();
+            double2 vv[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) vv[i] = fftb[t + T * i];
+            wave_lds_sync();
+            fft_block_wave<LOGN, -1>(vv, t, tw9, fftb);  // Z (unrotated)
+            const double2 pz = t < a.P ? fftb[lds_swz(pbin)] : make_double2(0.0, 0.0);
+            double2 dz[4];
+            double2 bacc = make_double2(a.pilot_ampl * pz.x, a.pilot_ampl * pz.y);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                dz[u] = t + T * u < a.D ? fftb[lds_swz(dbin[u])] : make_double2(0.0, 0.0);
+                bacc = cadd(bacc, cconj_mul(mpre[u], dz[u]));
+            }
+            const double isn = 1.0 / sqrt((double)N);
+            acc = cadd(acc, make_double2(bacc.x * isn, bacc.y * isn));
+            acc = block_sum2<T>(acc, red);
+            phr = atan2(acc.y, acc.x);
+            double rs2, rc2;
+            sincos(-phr, &rs2, &rc2);
+            const double2 rot = make_double2(rc2, rs2);
+            if (t < a.P) pil[t] = cmul_exact(pz, rot);
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                if (t + T * u < half) dat[t + T * u] = cmul_exact(dz[u], rot);
+        }
+        wave_lds_sync();
+        double acc = 0.0;
+        for (int i = t; i < a.P; i += T) acc += hypot(pil[i].x, pil[i].y);
+        acc = block_sum2<T>(make_double2(acc, 0.0), red).x;
+        const double phys = acc / ((double)a.P * a.pilot_ampl);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int i = t + T * u;
+            if (i < half) {
+                const int j = dslot[u];
+                const double2 p0 = make_double2(pil[j].x / phys, pil[j].y / phys);
+                const double2 coef = cdiv_exact(p0, p0);
+                const double2 fs = make_double2(dat[i].x / phys, dat[i].y / phys);
+                const double2 q = cdiv_exact(cdiv_exact(fs, coef), mpre[u]);
+                ph[i] = atan2(q.y, q.x);
+            }
+        }
+        wave_lds_sync();
+        unwrap_scan<T, true>(ph, half, reinterpret_cast<unsigned*>(red + 24));  // one-pass unwrap (Frame.hpp:407-414)
+        double sxy = 0.0, sy = 0.0;
+        for (int i = t; i < half; i += T) {
+            sxy += ph[i] * i;
+            sy += ph[i];
+        }
+        const double2 sums = block_sum2<T>(make_double2(sxy, sy), red + 16);
+        const double hn = (double)half;
+        const double sx = hn * (hn - 1) / 2, sx2 = (hn - 1) * hn * (2 * hn - 1) / 6;
+        const double b = (sums.x - sx * sums.y) / (sx2 - sx * sx);
+        if (t == 0) {
+            scal[1] = phr;
+            scal[2] = b;
+            scal[3] = sums.y - b * sx;
+        }
+    } else {
+        // ---------------------------------------------------------- message CP sums (wave 1)
+        // two symbols per iteration, so both symbols' CP loads are in flight together
+        const int t = lane;
+        for (int q = 1; q < Q; q += 2) {
+            const bool two = q + 1 < Q;  // uniform
+            double2 acc0 = make_double2(0.0, 0.0), acc1 = make_double2(0.0, 0.0);
+#pragma unroll 2
+            for (int j = t; j < a.cp; j += T) {
+                const long i0 = x0 + (long)q * L + j, i1 = two ? i0 + L : i0;
+                const double2 a0 = src_sample(a.iq, a.iq16, i0), b0 = src_sample(a.iq, a.iq16, i0 + N);
+                const double2 a1 = src_sample(a.iq, a.iq16, i1), b1 = src_sample(a.iq, a.iq16, i1 + N);
+                acc0 = cadd(acc0, cconj_mul(a0, b0));
+                acc1 = cadd(acc1, cconj_mul(a1, b1));
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                acc0.x += __shfl_xor(acc0.x, o);
+                acc0.y += __shfl_xor(acc0.y, o);
+                acc1.x += __shfl_xor(acc1.x, o);
+                acc1.y += __shfl_xor(acc1.y, o);
+            }
+            if (t == 0) {
+                cps[q] = acc0;
+                if (two) cps[q + 1] = acc1;
+            }
+        }
+    }
+    __syncthreads();  // cfo, phi[0], phr, the LS fit and the message CP sums visible
+    const double cfo = scal[0], phr = scal[1], b = scal[2], aa = scal[3];
+    {
+        double rs, rc;
+        sincospi(-2.0 * cfo * (double)N, &rs, &rc);
+        for (int q = 1 + tid; q < Q; q += 128) {
+            const double2 acc = cadd(make_double2(0.0, 0.0), cps[q]);
+            const double2 r = cmul_exact(acc, make_double2(rc, rs));
+            phi[q] = atan2(r.y, r.x);
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double acc = 0.0;
+        for (int q = 0; q < Q; ++q) {
+            psi[q] = acc;
+            acc += phi[q];
+        }
+    }
+    // chan_char_lq's line, as reciprocals for the rx multiply
+    double2* chan = a.chan_out + f * a.D;
+    for (int i = tid; i < a.D; i += 128) {
+        double th;
+        if (i < half)
+            th = add_rn(mul_rn(b, (double)i), aa);
+        else
+            th = add_rn(add_rn(mul_rn(-b, (double)a.D) / 2, mul_rn((double)(i - half), b)), aa);
+        double sn, cs;
+        sincos(th, &sn, &cs);
+        chan[i] = a.chan_recip ? cdiv_exact(make_double2(1.0, 0.0), make_double2(cs, sn)) : make_double2(cs, sn);
+    }
+    __syncthreads();  // psi visible
+    // message symbols: theta(m) = A_s + B_s m over the CP-stripped body
+    for (int s = tid; s < a.S; s += 128) {
+        const int q = 1 + s;
+        const double A = -2.0 * M_PI * cfo * (double)((long)q * L + a.cp) - (psi[q] * L + phi[q] * a.cp) / N - phr;
+        const double B = -2.0 * M_PI * cfo - phi[q] / N;
+        double sn, cs;
+        sincos(B * T, &sn, &cs);
+        double* o = a.corr_out + (f * a.S + s) * 4;
+        o[0] = A;
+        o[1] = B;
+        o[2] = cs;
+        o[3] = sn;
+    }
+}
+
+hipError_t launch_stream_sync(const CfoArgs& c, const StreamParamsArgs& a, int logn, int logm, int g, hipStream_t st)
+{
+    if (a.nframes <= 0) return hipSuccess;
+    const int L = (1 << logn) + a.cp;
+    if (logn != 9 || logm != 7 || g != 5 || L != 640 || a.npr != 1 || a.S + 1 > 64 || a.cp != 128 ||
+        a.D > 256 || a.P > 64 || c.P != a.P)
+        return hipErrorNotSupported;  // the two-kernel path covers other geometries
+    const size_t shm = sizeof(double2) * (TwLds<9>::SIZE + TwLds<7>::SIZE + 640 + a.P + (a.D / 2 + 1) + 32 + 1 + a.S) +
+                       sizeof(double) * (a.D / 2 + 2 + 64 + 64 + 4) + sizeof(int) * (a.P + 2);
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)stream_sync_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL(stream_sync_kernel, dim3((unsigned)a.nframes), dim3(128), shm, st, c, a);
+    return hipGetLastError();
 }
 
 // ========================================================================

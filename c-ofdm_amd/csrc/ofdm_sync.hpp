@@ -161,6 +161,9 @@ struct CompactArgs {
 hipError_t launch_compact(const CompactArgs& a, hipStream_t st);
 
 hipError_t launch_stream_params(int logn, const StreamParamsArgs& a, hipStream_t st);
+// pilot_freq_sinh + the params stage fused (N = 512, 640-point CFO form);
+// hipErrorNotSupported for other geometries (use launch_cfo + launch_stream_params)
+hipError_t launch_stream_sync(const CfoArgs& c, const StreamParamsArgs& a, int logn, int logm, int g, hipStream_t st);
 
 hipError_t launch_stream_walk(int logt, const WalkArgs& a, long nblocks, hipStream_t st);
 // stream walkers resident at once on the current device (occupancy of the
