@@ -484,12 +484,14 @@ __device__ __forceinline__ void fft_regs_tail_wave(double2 (&v)[8], int t, const
     }
 }
 
-// On entry v[i] = x[t + 64*i] (t = lane); on exit v[i] = X[t + 64*i].
+// On entry v[i] = x[t + T*i] (T = N/8 <= 64; for N < 512 a wave holds
+// 512/N transforms side by side, t the thread's index within its transform,
+// lds that transform's image); on exit v[i] = X[t + T*i].
 template <int LOGN, int SIGN>
 __device__ __forceinline__ void fft_regs_wave(double2 (&v)[8], int t, const double2* __restrict__ lds_tw,
                                               double2* __restrict__ lds)
 {
-    static_assert(LOGN == 9, "one wave = N/8 = 64 threads");
+    static_assert(LOGN >= 6 && LOGN <= 9, "N/8 <= one wave");
     stockham_pass<LOGN, 8, 1, SIGN>(v, t, lds_tw, lds);
     fft_regs_tail_wave<LOGN, 1, SIGN>(v, t, lds_tw, lds);
 }

@@ -1655,8 +1655,9 @@ __device__ int walk_preamble(const WalkArgs& a, long s, double2* xs, double2* c,
 //   |e^ - e| <= 1024 u ||x||_2 max|tspec|   (~10x the FFT-convolution bound,
 // (2 c log2 M + 1) u ||x|| ||tspec||_inf), and a window energy from two prefix
 // sums from the serial recurrence by (2L + 2i + 8) u (M + s_i) + (4R + 64) u P
-// (i: the lag from the search start; M: the largest window sum and sample
-// energy of every lag so far), so a lag clear of both thresholds by those
+// (i: the lag from the search start; M >= the largest window sum plus sample
+// energy of every lag so far: each window's total energy plus the largest
+// sample energy), so a lag clear of both thresholds by those
 // margins is decided as the reference decides it; the first lag that is not a
 // certain FAIL must be a certain PASS, else the exact search runs. The other
 // waves wait at the closing barrier (the transforms synchronise within the
@@ -1743,21 +1744,15 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
             // the image), so the decisions below run as a rolled loop
 #pragma unroll
             for (int j = 0; j < 8; ++j) buf[lane + 64 * j] = v[j];
-            // the largest window sum of this window's lags
-            double mloc = 0.0;
-#pragma unroll 1
-            for (int j = 0; j < 8; ++j) {
-                const int r = lane + 64 * j;
-                if (r < nl) mloc = fmax(mloc, P[r + L - 1] - (r ? P[r - 1] : 0.0));
-            }
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) mloc = fmax(mloc, __shfl_xor(mloc, o));
-            mrun = fmax(mrun, mloc);
+            // every window sum of this window's lags is at most its total
+            // energy (its samples lie inside the window): a bound on the
+            // largest window sum without a pass over the lags
+            mrun = fmax(mrun, ptot);
             erun = fmax(erun, emax);
             const double Mall = (mrun + erun) * 1.0625;
             const double scan_err = (4.0 * R + 64.0) * U * ptot;
             const double ef = 1024.0 * U * sqrt(ptot * 1.0625) * a.tspec_max;
-#pragma unroll 1
+#pragma unroll 2
             for (int j = 0; j < 8; ++j) {
                 const int r = lane + 64 * j, i = i0 + r;
                 int d = 0;  // 0 = certain FAIL, 1 = certain PASS, 2 = uncertain
@@ -1934,7 +1929,12 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
             // the last pass stays in registers: v[i] = X[tt + T*i], the bins
             // this thread sums (no final LDS write, barrier and re-read); the
             // image is next written after the bestg barriers below
-            fft_regs<LOGT, -1>(v, tt, lds_tw, fftb + g * N);
+            // a transform of T <= 64 threads lies within one wave: its LDS
+            // hand-offs need only wave-local syncs (no workgroup barrier)
+            if constexpr (T <= 64)
+                fft_regs_wave<LOGT, -1>(v, tt, lds_tw, fftb + g * N);
+            else
+                fft_regs<LOGT, -1>(v, tt, lds_tw, fftb + g * N);
             WPROF(const unsigned long long r1 = clock64();)
             double tot = 0.0, sine = 0.0;
 #pragma unroll
