@@ -1227,6 +1227,16 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     w.a2 = std::max(0, f2 - sm);
     w.b2 = std::min(c->t2 - 1, f2 + sm);
     w.t2_level = (double)c->p.t2_sin_level / 1000;
+    // FP32 T2 screen (certified, FP64 re-evaluation of uncertain steps).
+    // Test / experiment hooks: OFDM_WALK_T2_F32=0 turns it off,
+    // OFDM_WALK_T2_MARGIN overrides the certification margin (1 makes every
+    // block uncertain, i.e. every step is decided by the FP64 path).
+    {
+        const char* e32 = getenv("OFDM_WALK_T2_F32");
+        const char* em = getenv("OFDM_WALK_T2_MARGIN");
+        w.t2_f32 = !(e32 && e32[0] == '0');
+        w.t2_margin = em ? atof(em) : 4e-5;
+    }
     w.templ = c->d_templ;
     w.L = (int)c->p.pr_sin_len;
     w.cycles = (int)(2 * c->p.t2sin_size + c->p.pr_sin_len);

@@ -26,6 +26,7 @@
 #include <cstdint>
 
 #include "ofdm_fft.hpp"
+#include "ofdm_fft32.hpp"
 #include "ofdm_sync.hpp"
 
 // The sync chain mirrors the reference's x86-64 arithmetic (no FMA): no
@@ -1502,6 +1503,29 @@ __device__ __forceinline__ void load8_block(const A& a, long base, bool live, do
 
 __device__ __forceinline__ double energy_rn(double2 v) { return add_rn(mul_rn(v.x, v.x), mul_rn(v.y, v.y)); }
 
+// load8_block rounded to FP32 (int16 wire samples convert exactly).
+template <int T, class A>
+__device__ __forceinline__ void load8_block32(const A& a, long base, bool live, float2 (&v)[8])
+{
+    const long b0 = live ? base : 0;
+    if (a.iq16) {  // uniform
+        const int* p = reinterpret_cast<const int*>(a.iq16) + b0;
+        int w[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w[i] = p[T * i];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            v[i] = live ? make_float2((float)(short)(w[i] & 0xffff), (float)(w[i] >> 16)) : make_float2(0.f, 0.f);
+    } else {
+        const double2* p = a.iq + b0;
+        double2 d[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) d[i] = p[T * i];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = live ? make_float2((float)d[i].x, (float)d[i].y) : make_float2(0.f, 0.f);
+    }
+}
+
 // PREAMBLE_FORM::find_preamble from s: first lag with norm > 1 and
 // |sum_j x[s+i+j] c_j| / sqrt(norm) > level (Frame.cpp:338-378), INT_MAX if
 // none. Exact form: the running energy is the reference's serial recurrence
@@ -1839,7 +1863,7 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
     // T2 first-hit block, two slots used alternately (one barrier per scan
     // step), in scr[4] (the preamble search's answer is scr[2]): the
     // walker's LDS stays at 4 walkers per CU
-    int* bslot = reinterpret_cast<int*>(scr + 4);
+    int* bslot = reinterpret_cast<int*>(scr + 4);  // [0..1] first hit, [2..3] first uncertain (FP32 screen)
     double2* tw_m = reinterpret_cast<double2*>(scr + 16);  // TwLds<WALK_FFT_LOGM> (FFT search)
     double2* big = tw_m + TwLds<WALK_FFT_LOGM>::SIZE;
     double2* fftb = big;                                // G * N (T2 transforms)
@@ -1857,6 +1881,8 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
         *bestg = INT_MAX;
         bslot[0] = INT_MAX;
         bslot[1] = INT_MAX;
+        bslot[2] = INT_MAX;
+        bslot[3] = INT_MAX;
     }
     unsigned scan_it = 0;  // T2 scan steps so far (uniform): picks the bslot
     WPROF(unsigned long long p_t2 = 0, p_n2 = 0, p_pre = 0, p_np = 0, p_steps = 0;
@@ -1889,7 +1915,7 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
         // the walk loop and held live (register pressure sets the walkers per CU)
         int t;
         asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(t0));
-        const int g = t / T, tt = t - g * T;
+        const int g = t / T, tt0 = t - g * T;
         // The exit state is the first walk state at or past the core end, or
         // the state whose step located the first frame past it (a re-walk of
         // the next chunk starts there). The walk goes on until it
@@ -1901,41 +1927,32 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
             if (past || pos >= end + a.ext) break;
         }
         const long spos = pos;  // this step's start state
-        // find_t2sin(pos): blocks pos + k*N, G per step, first hit wins
+        // find_t2sin(pos): blocks pos + k*N, first hit wins
         long hit = -1;
         bool stop = false;
         WPROF(++p_steps; unsigned long long p_a = clock64();)
-        for (long base = pos;; base += (long)G * N) {
-            WPROF(++p_n2;)
-            if (base + N > a.n) {  // no full block left: the walk has consumed the stream
-                stop = true;
-                break;
-            }
-            if (base >= end) {  // scanning past the core: an equivalent state
-                if (exitp < 0) exitp = base;
-                // the end fell inside a scan: walk on to the next located frame
-                // (within ext_scan), so that the next chunk's walk, which
-                // locates it too, syncs with this one without a re-walk
-                if (base >= end + a.ext_scan) {
-                    stop = true;
-                    break;
-                }
-            }
+        // FP64: G blocks from `base` (block g per group of T threads); the
+        // first block whose ratio exceeds the level (Frame.hpp:150-197), or
+        // INT_MAX. Slot scan_it & 1 collects the first hit; the other slot was
+        // read before this evaluation's barrier and is reset for the next.
+        auto t2_eval64 = [&](long base) -> int {
+            // opaque per-evaluation copy of the thread's index in its group:
+            // the pass addresses and bin masks are derived here, not hoisted
+            // out of the scan and held live across it
+            int tt;
+            asm volatile("v_mov_b32 %0, %1" : "=v"(tt) : "v"(tt0));
             const long b = base + (long)g * N;
             const bool live = b + N <= a.n;
             double2 v[8];
             load8_block<T>(a, b + tt, live, v);
-            WPROF(const unsigned long long r0 = clock64();)
             // the last pass stays in registers: v[i] = X[tt + T*i], the bins
-            // this thread sums (no final LDS write, barrier and re-read); the
-            // image is next written after the bestg barriers below
-            // a transform of T <= 64 threads lies within one wave: its LDS
-            // hand-offs need only wave-local syncs (no workgroup barrier)
+            // this thread sums (no final LDS write, barrier and re-read); a
+            // transform of T <= 64 threads lies within one wave, so its LDS
+            // hand-offs need only wave-local syncs
             if constexpr (T <= 64)
                 fft_regs_wave<LOGT, -1>(v, tt, lds_tw, fftb + g * N);
             else
                 fft_regs<LOGT, -1>(v, tt, lds_tw, fftb + g * N);
-            WPROF(const unsigned long long r1 = clock64();)
             double tot = 0.0, sine = 0.0;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
@@ -1962,10 +1979,6 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
                     sine += red[g * NW + w].y;
                 }
             }
-            // slot scan_it & 1 collects this step's first hit. The other slot
-            // was read in the previous step, before this step's barrier, and
-            // is reset here for the next step, whose atomics come after the
-            // barriers inside its transform.
             int* hslot = bslot + (scan_it & 1);
             if (tt == 0 && live && tot != 0.0) {
                 const double rel = sine / tot;
@@ -1975,13 +1988,120 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
             const int bg = *hslot;
             if (t == 0) bslot[(scan_it + 1) & 1] = INT_MAX;
             ++scan_it;
-            WPROF(if (t == 0 && blockIdx.x < 8192) {
-                unsigned long long* q = g_walk_sub + 8 * blockIdx.x;
-                q[4] += r1 - r0; q[5] += clock64() - r1;
-            })
-            if (bg != INT_MAX) {
-                hit = base + (long)bg * N;
-                break;
+            return bg;
+        };
+        // stop checks of a scan step from `base` (the walk state is `base`)
+        auto scan_stop = [&](long base) -> bool {
+            if (base + N > a.n) return true;  // no full block left: the walk has consumed the stream
+            if (base >= end) {                // scanning past the core: an equivalent state
+                if (exitp < 0) exitp = base;
+                // the end fell inside a scan: walk on to the next located frame
+                // (within ext_scan), so that the next chunk's walk, which
+                // locates it too, syncs with this one without a re-walk
+                if (base >= end + a.ext_scan) return true;
+            }
+            return false;
+        };
+        if constexpr (T <= 64) {
+            if (a.t2_f32) {
+                // FP32 screen of 2G blocks per scan step (blocks g and g + G per
+                // group): half the registers and LDS of an FP64 block, so twice
+                // the blocks per step at the FP64 step's cost, fewer steps per
+                // frame. Certified per block: FP32 energies in the normal range
+                // and a ratio clear of the level by t2_margin (>= 4x the bound
+                // of the FP32 transform and sums) decide as FP64
+                // does; when the first block that is not a certain FAIL is
+                // uncertain, the step is evaluated again in FP64.
+                float2* fftb32 = reinterpret_cast<float2*>(big);
+                const float lev = (float)a.t2_level, marg = (float)a.t2_margin;
+                for (long base = pos;; base += 2L * G * N) {
+                    WPROF(++p_n2;)
+                    if (scan_stop(base)) {
+                        stop = true;
+                        break;
+                    }
+                    int tt;  // opaque per-step copy (see t2_eval64)
+                    asm volatile("v_mov_b32 %0, %1" : "=v"(tt) : "v"(tt0));
+                    const long bA = base + (long)g * N, bB = bA + (long)G * N;
+                    const bool liveA = bA + N <= a.n, liveB = bB + N <= a.n;
+                    float2 va[8], vb[8];
+                    load8_block32<T>(a, bA + tt, liveA, va);
+                    load8_block32<T>(a, bB + tt, liveB, vb);
+                    fft_regs_wave32<LOGT, -1>(va, tt, lds_tw, fftb32 + g * N);
+                    fft_regs_wave32<LOGT, -1>(vb, tt, lds_tw, fftb32 + (g + G) * N);
+                    float ta = 0.f, sa = 0.f, tb = 0.f, sb = 0.f;
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const int k = tt + T * i;
+                        const float m = (float)((k >= a.a1 && k <= a.b1) + (k >= a.a2 && k <= a.b2));
+                        const float ea = va[i].x * va[i].x + va[i].y * va[i].y;
+                        const float eb = vb[i].x * vb[i].x + vb[i].y * vb[i].y;
+                        ta += ea;
+                        sa += m * ea;
+                        tb += eb;
+                        sb += m * eb;
+                    }
+                    constexpr int W0 = T / 2;
+#pragma unroll
+                    for (int o = W0; o > 0; o >>= 1) {
+                        ta += __shfl_xor(ta, o);
+                        sa += __shfl_xor(sa, o);
+                        tb += __shfl_xor(tb, o);
+                        sb += __shfl_xor(sb, o);
+                    }
+                    // 0 = certain FAIL, 1 = certain PASS, 2 = uncertain
+                    auto screen = [&](bool live, float tot, float sine) -> int {
+                        if (!live) return 0;
+                        if (!(tot >= 1e-20f && tot <= 1e30f)) return 2;  // zero, tiny, huge or NaN: FP64 decides
+                        const float rel = sine / tot;
+                        if (rel > lev + marg) return 1;
+                        if (rel <= lev - marg) return 0;
+                        return 2;
+                    };
+                    int* hslot = bslot + (scan_it & 1);
+                    int* uslot = bslot + 2 + (scan_it & 1);
+                    if (tt == 0) {
+                        const int da = screen(liveA, ta, sa), db = screen(liveB, tb, sb);
+                        if (da) atomicMin(hslot, g);
+                        if (da == 2) atomicMin(uslot, g);
+                        if (db) atomicMin(hslot, g + G);
+                        if (db == 2) atomicMin(uslot, g + G);
+                    }
+                    __syncthreads();
+                    int bg = *hslot;
+                    const int bu = *uslot;
+                    if (t == 0) {
+                        bslot[(scan_it + 1) & 1] = INT_MAX;
+                        bslot[2 + ((scan_it + 1) & 1)] = INT_MAX;
+                    }
+                    ++scan_it;
+                    if (bg != INT_MAX && bu == bg) {  // uniform: this step's decision in FP64
+                        WPROF(if (t == 0) atomicAdd(&g_walk_fallbacks, 1ULL << 32));
+                        bg = t2_eval64(base);
+                        if (bg == INT_MAX) {
+                            bg = t2_eval64(base + (long)G * N);
+                            if (bg != INT_MAX) bg += G;
+                        }
+                    }
+                    if (bg != INT_MAX) {
+                        hit = base + (long)bg * N;
+                        break;
+                    }
+                }
+            }
+        }
+        if (!(T <= 64 && a.t2_f32)) {
+            for (long base = pos;; base += (long)G * N) {
+                WPROF(++p_n2;)
+                if (scan_stop(base)) {
+                    stop = true;
+                    break;
+                }
+                const int bg = t2_eval64(base);
+                if (bg != INT_MAX) {
+                    hit = base + (long)bg * N;
+                    break;
+                }
             }
         }
         WPROF(unsigned long long p_b = clock64(); p_t2 += p_b - p_a;)

@@ -81,6 +81,8 @@ struct WalkArgs {
     const double2* t2tw;        // T2sin_size forward twiddles
     int a1, b1, a2, b2;         // T2 mask bands
     double t2_level;
+    int t2_f32;                 // screen T2 blocks in FP32 (certified; T2sin_size <= 512)
+    double t2_margin;           // FP32 screen: certain when |ratio - level| > t2_margin
     const double2* templ;       // pr_sin_len conj template
     int L, cycles;              // pr_sin_len, 2*T2sin_size + pr_sin_len
     double pr_level;

@@ -106,6 +106,26 @@ def test_stream_walk_certified_search_equals_serial_recurrence(monkeypatch):
         assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("env", [{"OFDM_WALK_T2_MARGIN": "1"}, {"OFDM_WALK_T2_F32": "0"}, {"OFDM_WALK_T2_MARGIN": "0"}])
+def test_stream_walk_fp32_t2_screen_equals_fp64(monkeypatch, env):
+    # the walker's certified FP32 T2 screen against FP64 only: margin 1 makes
+    # every block uncertain (each scan step re-evaluated by the FP64 path),
+    # OFDM_WALK_T2_F32=0 is the FP64 scan, margin 0 trusts the raw FP32
+    # ratios (still equal on this stream: no block within 1e-5 of the level)
+    for cfg, nf, seed in ((D, 40, 4), (dict(D, fft_size=256, num_data_subc=128, num_pilot_subc=8, cp_size=64), 30, 6)):
+        x, data = impaired_stream(cfg, nf, seed=seed)
+        screened = run_stream(cfg, x, chunk=9000)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        other = run_stream(cfg, x, chunk=9000)
+        for k in env:
+            monkeypatch.delenv(k)
+        assert screened[0] == other[0]
+        for a, b in zip(screened[1:], other[1:]):
+            assert np.array_equal(a, b)
+        check_against_oracle(cfg, x, screened)
+
+
 def test_stream_unfused_decode_path():
     # num_symb = 12 exceeds the rx register window, so the located frames take
     # the gather + staged sync chain + staged rx path instead of the fused decode
