@@ -1332,20 +1332,6 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
             sa.cp = c->cp;
             sa.pilot_ampl = (double)c->p.pilot_ampl / 1000;
             sa.count = d_cnt;
-            // one kernel for pilot_freq_sinh + the params stage where the
-            // geometry allows (N = 512, 640-point CFO form), else two
-            hipError_t e2 = hipErrorNotSupported;
-#ifndef OFDM_STREAM_SYNC2  // timing experiment only: the two-kernel path
-            e2 = ofdm::launch_stream_sync(ca, sa, c->logn, pl->logm, pl->g, st);
-#endif
-            if (e2 == hipErrorNotSupported) {
-                e2 = ofdm::launch_cfo(pl->logm, pl->g, ca, st);
-                if (e2 != hipSuccess) return hip_fail(e2, "stream cfo launch");
-                e2 = ofdm::launch_stream_params(c->logn, sa, st);
-                if (e2 != hipSuccess) return hip_fail(e2, "stream params launch");
-            } else if (e2 != hipSuccess) {
-                return hip_fail(e2, "stream sync launch");
-            }
             ofdm::RxArgs ra{};
             ra.tab = c->tables(false);
             ra.iq = reinterpret_cast<const double2*>(iq);
@@ -1371,8 +1357,34 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
             // static frame order: the next frame's symbol 0 is fetched ahead of
             // the gains (stream rx 500 -> 416 us with the queue's late fetch)
             ra.queue = nullptr;
-            e2 = ofdm::launch_rx(c->logn, ra, st, nullptr);
-            if (e2 != hipSuccess) return hip_fail(e2, "stream rx launch");
+            // One kernel for the whole decode where the geometry allows (N =
+            // 512, 640-point CFO form: sync stage + rx stage per frame, the
+            // ramps and channel through LDS); else pilot_freq_sinh + the
+            // params stage (one kernel or two), then the stream rx.
+            hipError_t e2 = hipErrorNotSupported;
+#ifndef OFDM_STREAM_SYNC2  // timing experiment only: the staged launches
+            e2 = ofdm::launch_stream_decode(ca, sa, ra, c->logn, pl->logm, pl->g, st);
+#endif
+            if (e2 == hipErrorNotSupported) {
+                // one kernel for pilot_freq_sinh + the params stage where the
+                // geometry allows (N = 512, 640-point CFO form), else two
+                e2 = hipErrorNotSupported;
+#ifndef OFDM_STREAM_SYNC2  // timing experiment only: the two-kernel path
+                e2 = ofdm::launch_stream_sync(ca, sa, c->logn, pl->logm, pl->g, st);
+#endif
+                if (e2 == hipErrorNotSupported) {
+                    e2 = ofdm::launch_cfo(pl->logm, pl->g, ca, st);
+                    if (e2 != hipSuccess) return hip_fail(e2, "stream cfo launch");
+                    e2 = ofdm::launch_stream_params(c->logn, sa, st);
+                    if (e2 != hipSuccess) return hip_fail(e2, "stream params launch");
+                } else if (e2 != hipSuccess) {
+                    return hip_fail(e2, "stream sync launch");
+                }
+                e2 = ofdm::launch_rx(c->logn, ra, st, nullptr);
+                if (e2 != hipSuccess) return hip_fail(e2, "stream rx launch");
+            } else if (e2 != hipSuccess) {
+                return hip_fail(e2, "stream decode launch");
+            }
         }
         return OFDM_OK;
     };

@@ -18,8 +18,10 @@
 #include <cstdint>
 #include <cstdlib>
 
+#include "ofdm_dev.hpp"
 #include "ofdm_fft.hpp"
 #include "ofdm_internal.hpp"
+#include "ofdm_rx2.hpp"
 
 #include <type_traits>
 
@@ -40,24 +42,6 @@ __device__ __forceinline__ int symbol_bits(const uint8_t* __restrict__ b, long n
     return (w >> (16 - off - k)) & mask;
 }
 
-// Modulation::demod decision for one point (modulation.cpp:62-84): BPSK
-// re+im > 0; QAM clamp to [-1,1] then uint8((v+1)*str_size_1 + 0.5) per axis,
-// idx = re | im*str_size. Separate roundings (no FMA) as on x86-64.
-// The clamp is v_max/v_min: equal to the reference's compare chain for every
-// non-NaN value; a NaN (degenerate all-zero pilots) decides 0 either way
-// (chain: cvt(NaN) = 0; min/max: clamps to -1, then uint8(0.5) = 0).
-// decide() as a select (no branch on k): the same value for every k.
-__device__ __forceinline__ int decide_select(double2 z, int k, double s1, int m)
-{
-    const double re = __builtin_fmin(__builtin_fmax(z.x, -1.0), 1.0);
-    const double im = __builtin_fmin(__builtin_fmax(z.y, -1.0), 1.0);
-    const int ire = (uint8_t)(int)add_rn(mul_rn(add_rn(re, 1.0), s1), 0.5);
-    const int iim = (uint8_t)(int)add_rn(mul_rn(add_rn(im, 1.0), s1), 0.5);
-    const int qam = (ire | (iim * m)) & 0xff;
-    const int bpsk = (z.x + z.y) > 0.0;
-    return k == 1 ? bpsk : qam;
-}
-
 __device__ __forceinline__ int decide(double2 z, int k, double s1, int m)
 {
     if (k == 1) return (z.x + z.y) > 0.0;
@@ -66,32 +50,6 @@ __device__ __forceinline__ int decide(double2 z, int k, double s1, int m)
     const int ire = (uint8_t)(int)add_rn(mul_rn(add_rn(re, 1.0), s1), 0.5);
     const int iim = (uint8_t)(int)add_rn(mul_rn(add_rn(im, 1.0), s1), 0.5);
     return (ire | (iim * m)) & 0xff;
-}
-
-// Four output bytes (one little-endian word) from 32/K consecutive K-bit
-// decisions held one per byte in LDS (MSB-first within each byte, as
-// bit_stream_converter(8, K, ...), modulation.cpp:90-125).
-template <int K>
-__device__ __forceinline__ uint32_t pack_word(const uint8_t* __restrict__ dec)
-{
-    constexpr int PER = 8 / K;  // decisions per output byte
-    constexpr int NW = 8 / K;   // 32-bit LDS words holding the 32/K decisions (dec is 32/K-byte aligned)
-    uint32_t d[NW];
-    const uint32_t* d32 = reinterpret_cast<const uint32_t*>(dec);
-#pragma unroll
-    for (int i = 0; i < NW; ++i) d[i] = d32[i];
-    uint32_t word = 0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        uint32_t byte = 0;
-#pragma unroll
-        for (int r = 0; r < PER; ++r) {
-            const int idx = b * PER + r;
-            byte = (byte << K) | ((d[idx >> 2] >> (8 * (idx & 3))) & 0xffu);
-        }
-        word |= byte << (8 * b);
-    }
-    return word;
 }
 
 __device__ __forceinline__ double2 clamp_point(double2 z)
@@ -154,17 +112,6 @@ __device__ __forceinline__ double2 awgn_sample(const AwgnRun& run, uint32_t j, d
 
 __device__ __forceinline__ int16_t to_int16(double v) { return (int16_t)(int)v; }
 
-// Streams touched once (tx output, rx input, constellation output): non-temporal
-// 16-B accesses, so a launch neither evicts the caches for nothing nor leaves
-// gigabytes of dirty lines for the next launch to write back.
-typedef double nt_double2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ void store_nt(double2* p, double2 v)
-{
-    nt_double2 w = {v.x, v.y};
-    __builtin_nontemporal_store(w, reinterpret_cast<nt_double2*>(p));
-}
-
 // A global load the compiler's wait-count pass does not track: issued and
 // waited for (vmcnt(0)) inside one asm block. For rare paths (e.g. channel
 // carriers that do not fit LDS) inside code that otherwise issues only
@@ -176,12 +123,6 @@ __device__ __forceinline__ double2 load_untracked(const double2* p)
     double2 v;
     asm volatile("global_load_dwordx4 %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
     return v;
-}
-
-__device__ __forceinline__ double2 load_nt(const double2* p)
-{
-    const nt_double2 w = __builtin_nontemporal_load(reinterpret_cast<const nt_double2*>(p));
-    return make_double2(w.x, w.y);
 }
 
 template <int NT>
@@ -942,186 +883,36 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
 }
 
 // ------------------------------------------------------------------ stream rx, two waves per frame
-// rx_kernel's stream mode (SYNC) for N = 512, where one transform is one
-// wave: the frame's message symbols are split over two waves, wave w
-// transforming s = w, w + 2, ..., so each wave holds half of the frame's
-// register window (RX_SMAX/2 symbols x RX_DPT carriers = 64 VGPRs) and the
-// kernel runs 3 waves per SIMD (155 VGPRs; rx_kernel: 2 at 256), 6 frames
-// per CU each transformed by two waves at once (LDS: one image per wave; the
-// transforms sync within their wave). No prefetch registers: the other waves
-// of the SIMD cover the load latency.
-// The arithmetic is rx_kernel's, operation for operation: the phase ramp,
-// the transform, phys (wave 0, the same lane order), the gains, the channel
-// reciprocal multiply (the fused stream decode's chan_recip mode; D <= 256),
-// the decisions.
+// rx_kernel's stream mode (SYNC) for N = 512 (one transform = one wave),
+// persistent over the located frames: each frame's channel reciprocals to
+// LDS, then rx2_frame (ofdm_rx2.hpp: two waves per frame, 3 waves/SIMD).
 template <bool I16>
 __global__ void __launch_bounds__(128, 3) rx_stream2_kernel(RxArgs a)
 {
-    constexpr int LOGN = 9, N = 512, T = 64, SH = RX_SMAX / 2;
+    constexpr int LOGN = 9, N = 512, T = 64;
     extern __shared__ double2 smem[];
     const int S = a.S, D = a.D, P = a.P;
-    double2* lds_tw = smem + 2 * N;                          // TwLds::SIZE
-    double2* pil = lds_tw + TwLds<LOGN>::SIZE;               // S*P raw pilots
-    double2* gain = pil + S * P;                             // S*P equaliser gains
-    double* red = reinterpret_cast<double*>(gain + S * P);   // phys
-    uint8_t* dec = reinterpret_cast<uint8_t*>(smem);         // S*D decisions: the images, after the transforms
+    Rx2Lds L;
+    L.img = smem;                                            // 2 * N
+    L.tw = smem + 2 * N;                                     // TwLds::SIZE
+    L.pil = L.tw + TwLds<LOGN>::SIZE;                        // S*P raw pilots
+    L.gain = L.pil + S * P;                                  // S*P equaliser gains
+    L.chl = L.gain + S * P;                                  // D channel reciprocals
+    L.red = reinterpret_cast<double*>(L.chl + D);            // phys
     const int tid = threadIdx.x, lane0 = tid & 63;
     const long nfr = a.count ? min(*a.count, a.nframes) : a.nframes;
     if ((long)blockIdx.x >= nfr) return;  // uniform
-    load_twiddles<LOGN>(a.tab.tw, lds_tw, tid, 128);
+    load_twiddles<LOGN>(a.tab.tw, L.tw, tid, 128);
     int pk[RX_DPT];
 #pragma unroll
     for (int i = 0; i < RX_DPT; ++i) pk[i] = a.tab.rx_pack[lane0 + T * i];
     const int pbin = a.tab.pilot_swz[lane0];
-    const int m = 1 << (a.k / 2);
-    const double s1 = a.k == 1 ? 0.0 : 1.0 / (2.0 / (m - 1));
-    const long bpf = a.bytes_per_frame;
-    const bool by_word = (a.k == 1 || a.k == 2 || a.k == 4 || a.k == 8) && (bpf & 3) == 0 &&
-                         ((uintptr_t)a.bytes & 3) == 0;
-    const int L = N + a.cp;
-    __syncthreads();  // twiddles visible
 #pragma unroll 1
     for (long f = blockIdx.x; f < nfr; f += gridDim.x) {
-        // opaque per-frame copies: addresses derived from them are recomputed
-        // per frame, not held live beside the register window
-        int lane;
-        asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(lane0));
-#pragma unroll
-        for (int i = 0; i < RX_DPT; ++i) asm volatile("" : "+v"(pk[i]));
-        const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-        double2* img = smem + w * N;
-        const long x0 = a.starts[f] + a.start_off;
-        double2 y[SH][RX_DPT];
-        // the wave's symbols, unrolled (compile-time window registers); each
-        // starts from an opaque lane copy and a memory fence, so nothing of one
-        // symbol (loads, LDS addresses) is hoisted and held across another
-#pragma unroll
-        for (int q = 0; q < SH; ++q) {
-            const int s = 2 * q + w;
-            if (s < S) {  // uniform
-                asm volatile("" ::: "memory");
-                int lq;
-                asm volatile("v_mov_b32 %0, %1" : "=v"(lq) : "v"(lane));
-                // the ramp's start phasor first (its sincos temporaries die
-                // before the sample registers are allocated)
-                const double* cr = a.corr + (f * S + s) * 4;
-                double sn, cs;
-                sincos(cr[0] + cr[1] * (double)lq, &sn, &cs);
-                double2 c = make_double2(cs, sn);
-                const double2 wr = make_double2(cr[2], cr[3]);
-                asm volatile("" ::: "memory");
-                double2 v[8];
-                const long off = x0 + (long)s * L + lq;
-                if constexpr (I16) {
-                    const int* p = reinterpret_cast<const int*>(a.iq16 + off);
-                    int r[8];
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) r[i] = __builtin_nontemporal_load(p + T * i);
-#pragma unroll
-                    for (int i = 0; i < 8; ++i)
-                        v[i] = make_double2((double)(int)(short)(r[i] & 0xffff), (double)(r[i] >> 16));
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) v[i] = load_nt(a.iq + off + T * i);
-                }
-                // sample m = lq + T*i of the body: *= e^{i(A + B m)}, by a
-                // running product from e^{i(A + B lq)} in steps of e^{i B T}
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    v[i] = cmul(v[i], c);
-                    if (i < 7) c = cmul(c, wr);
-                }
-                fft_block_wave<LOGN, -1>(v, lq, lds_tw, img);
-                if (lq < P) pil[s * P + lq] = img[pbin];
-#pragma unroll
-                for (int i = 0; i < RX_DPT; ++i) y[q][i] = img[pk[i] & 0xffff];
-                wave_lds_sync();  // read before the next transform rewrites the image
-            }
-        }
-        __syncthreads();  // both waves' pilots visible; the images are free
-        // the frame's channel reciprocals (main.cpp:69-71's divisors) to LDS,
-        // past the decisions in the free images; requested now, stored after
-        // the gains (the emit's stores would queue in front of loads issued there)
-        double2* chl = reinterpret_cast<double2*>(smem) + ((S * D + 15) >> 4);
         const double2* chan = a.chan + f * a.chan_stride;
-        double2 chv[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {  // D <= 256 = 2 x 128
-            const int d = tid + 128 * u;
-            chv[u] = chan[d < D ? d : 0];
-        }
-        // phys_pilot_ampl = sum |pilot| / (P*S*pilot_ampl)   (Frame.cpp:76-80),
-        // summed by wave 0 in rx_kernel's lane order
-        if (w == 0) {
-            double acc = 0.0;
-            for (int i = lane; i < S * P; i += T) acc += hypot(pil[i].x, pil[i].y);
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-            if (lane == 0) red[0] = acc;
-        }
-        __syncthreads();
-        const double phys = red[0] / ((double)(P * S) * a.pilot_ampl);
-        // out = (F/phys) / ((F[s,p]/phys) / (F[0,p]/phys)) = F * gain[s][j]   (Frame.cpp:82-93)
-        for (int i = tid; i < S * P; i += 128) {
-            const int j = i % P;
-            const double2 c0 = make_double2(pil[j].x / phys, pil[j].y / phys);
-            const double2 cs = make_double2(pil[i].x / phys, pil[i].y / phys);
-            const double2 coef = cdiv_exact(cs, c0);
-            const double2 g = cdiv_exact(make_double2(1.0, 0.0), coef);
-            gain[i] = make_double2(g.x / phys, g.y / phys);
-        }
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-            if (tid + 128 * u < D) chl[tid + 128 * u] = chv[u];
-        __syncthreads();
-        auto emit = [&](int s, const double2 (&yw)[RX_DPT]) {
-            double2* cbase = a.constell ? a.constell + (f * S + s) * D : nullptr;
-#pragma unroll
-            for (int i = 0; i < RX_DPT; ++i) {
-                int d = lane + T * i, gi = s * P + (pk[i] >> 16);
-                asm volatile("" : "+v"(d), "+v"(gi));  // opaque: not hoisted and held
-                if (d < D) {
-                    double2 o = cmul_exact(yw[i], gain[gi]);
-                    o = cmul_exact(o, chl[d]);  // chan_recip (host-checked)
-                    if (cbase) store_nt(cbase + d, o);
-                    dec[s * D + d] = (uint8_t)decide_select(o, a.k, s1, m);
-                }
-            }
-        };
-#pragma unroll
-        for (int q = 0; q < SH; ++q) {
-            const int s = 2 * q + w;
-            if (s < S) emit(s, y[q]);  // uniform
-        }
-        __syncthreads();  // decisions visible
-        if (a.bytes) {
-            if (by_word) {
-                const int per_word = 32 / a.k;  // decisions per output word
-                for (long wd = tid; wd < bpf / 4; wd += 128) {
-                    const uint8_t* dw = dec + wd * per_word;
-                    uint32_t word;
-                    switch (a.k) {
-                        case 1: word = pack_word<1>(dw); break;
-                        case 2: word = pack_word<2>(dw); break;
-                        case 4: word = pack_word<4>(dw); break;
-                        default: word = pack_word<8>(dw); break;
-                    }
-                    reinterpret_cast<uint32_t*>(a.bytes + f * bpf)[wd] = word;
-                }
-            } else {
-                for (long jb = tid; jb < bpf; jb += 128) {
-                    int byte = 0;
-                    for (int b = 0; b < 8; ++b) {
-                        const long bit = jb * 8 + b;
-                        const long g = bit / a.k;
-                        const int within = (int)(bit % a.k);
-                        byte = (byte << 1) | ((dec[g] >> (a.k - 1 - within)) & 1);
-                    }
-                    a.bytes[f * bpf + jb] = (uint8_t)byte;
-                }
-            }
-        }
-        __syncthreads();  // dec / pil / gain are rewritten by the next frame
+        for (int d = tid; d < D; d += 128) L.chl[d] = chan[d];
+        __syncthreads();  // twiddles (first frame) and the channel visible
+        rx2_frame<I16>(a, f, L, a.corr + f * S * 4, pk, pbin);
     }
 }
 
@@ -1320,7 +1111,7 @@ static hipError_t rx_launch_n(const RxArgs& a, hipStream_t st)
 template <bool I16>
 static hipError_t rx_stream2_launch(const RxArgs& a, hipStream_t st)
 {
-    const size_t shm = sizeof(double2) * (2 * 512 + TwLds<9>::SIZE + 2 * (size_t)a.S * a.P) + 2 * sizeof(double);
+    const size_t shm = sizeof(double2) * (2 * 512 + TwLds<9>::SIZE + 2 * (size_t)a.S * a.P + a.D) + 2 * sizeof(double);
     if (shm > 160 * 1024) return hipErrorInvalidValue;
     static bool attr = false;
     if (!attr) {

@@ -1,0 +1,204 @@
+// ofdm_rx2.hpp — the stream rx stage for N = 512 with two waves per frame
+// (rx_kernel's stream mode, main.cpp:67-71 + FFT_FORM::read Frame.cpp:73-96
+// + Modulation::demod modulation.cpp:53-87 on a located frame whose
+// freq_shift / cp_freq_sinh / pr_phase_sinh corrections are two ramp numbers
+// per symbol). Used by rx_stream2_kernel (ofdm_kernels.hip) and by the fused
+// stream decode (ofdm_sync.hip stream_decode_kernel). Included before any
+// `#pragma clang fp contract(off)`: the arithmetic is rx_kernel's.
+//
+// The frame's message symbols are split over two waves, wave w transforming
+// s = w, w + 2, ..., so each wave holds half of the frame's register window
+// (RX_SMAX/2 symbols x RX_DPT carriers = 64 VGPRs): 3 waves per SIMD (rx_kernel:
+// 2 at 256 VGPRs), each frame transformed by two waves at once (one LDS
+// image per wave; the transforms sync within their wave). No prefetch
+// registers: the other waves of the SIMD cover the load latency. The
+// operations are rx_kernel's, one for one: the phase ramp, the transform,
+// phys (wave 0, the same lane order), the gains, the channel reciprocal
+// multiply (chan_recip mode; D <= 256), the decisions.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "ofdm_dev.hpp"
+#include "ofdm_fft.hpp"
+#include "ofdm_internal.hpp"
+
+namespace ofdm {
+
+struct Rx2Lds {
+    double2* img;   // 2 * 512: one transform image per wave; the S*D decisions over them afterwards
+    double2* tw;    // TwLds<9>
+    double2* pil;   // S*P raw pilots
+    double2* gain;  // S*P equaliser gains
+    double2* chl;   // D channel reciprocals: filled and visible on entry, or (chan_g) staged
+                    // here from global after the transforms (then over the images, past the
+                    // S*D decisions)
+    double* red;    // phys
+};
+
+// Frame f of a.starts (message body at starts[f] + start_off); corr: its S*4
+// ramp numbers {A, B, cos(B*T), sin(B*T)} (global or LDS); chan_g: nullptr,
+// or the frame's D channel reciprocals in global memory, requested after the
+// transforms and stored to L.chl after the gains (loads issued among the
+// emit's stores would wait for them). Every thread of the 128-thread
+// workgroup calls it; it returns after a barrier (LDS reusable).
+template <bool I16>
+__device__ __forceinline__ void rx2_frame(const RxArgs& a, long f, const Rx2Lds& L, const double* corr,
+                                          const int (&pk0)[RX_DPT], int pbin, const double2* chan_g = nullptr)
+{
+    constexpr int LOGN = 9, N = 512, T = 64, SH = RX_SMAX / 2;
+    const int S = a.S, D = a.D, P = a.P;
+    const int tid = threadIdx.x;
+    const int m = 1 << (a.k / 2);
+    const double s1 = a.k == 1 ? 0.0 : 1.0 / (2.0 / (m - 1));
+    const long bpf = a.bytes_per_frame;
+    const bool by_word = (a.k == 1 || a.k == 2 || a.k == 4 || a.k == 8) && (bpf & 3) == 0 &&
+                         ((uintptr_t)a.bytes & 3) == 0;
+    const int Lf = N + a.cp;
+    uint8_t* dec = reinterpret_cast<uint8_t*>(L.img);
+    // opaque per-frame copies: addresses derived from them are recomputed per
+    // frame, not held live beside the register window
+    int lane;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(tid & 63));
+    int pk[RX_DPT];
+#pragma unroll
+    for (int i = 0; i < RX_DPT; ++i) {
+        pk[i] = pk0[i];
+        asm volatile("" : "+v"(pk[i]));
+    }
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    double2* img = L.img + w * N;
+    const long x0 = a.starts[f] + a.start_off;
+    double2 y[SH][RX_DPT];
+    // the wave's symbols, unrolled (compile-time window registers); each
+    // starts from an opaque lane copy and a memory fence, so nothing of one
+    // symbol (loads, LDS addresses) is hoisted and held across another
+#pragma unroll
+    for (int q = 0; q < SH; ++q) {
+        const int s = 2 * q + w;
+        if (s < S) {  // uniform
+            asm volatile("" ::: "memory");
+            int lq;
+            asm volatile("v_mov_b32 %0, %1" : "=v"(lq) : "v"(lane));
+            // the ramp's start phasor first (its sincos temporaries die
+            // before the sample registers are allocated)
+            const double* cr = corr + s * 4;
+            double sn, cs;
+            sincos(cr[0] + cr[1] * (double)lq, &sn, &cs);
+            double2 c = make_double2(cs, sn);
+            const double2 wr = make_double2(cr[2], cr[3]);
+            asm volatile("" ::: "memory");
+            double2 v[8];
+            const long off = x0 + (long)s * Lf + lq;
+            if constexpr (I16) {
+                const int* p = reinterpret_cast<const int*>(a.iq16 + off);
+                int r[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) r[i] = __builtin_nontemporal_load(p + T * i);
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    v[i] = make_double2((double)(int)(short)(r[i] & 0xffff), (double)(r[i] >> 16));
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v[i] = load_nt(a.iq + off + T * i);
+            }
+            // sample m = lq + T*i of the body: *= e^{i(A + B m)}, by a
+            // running product from e^{i(A + B lq)} in steps of e^{i B T}
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                v[i] = cmul(v[i], c);
+                if (i < 7) c = cmul(c, wr);
+            }
+            fft_block_wave<LOGN, -1>(v, lq, L.tw, img);
+            if (lq < P) L.pil[s * P + lq] = img[pbin];
+#pragma unroll
+            for (int i = 0; i < RX_DPT; ++i) y[q][i] = img[pk[i] & 0xffff];
+            wave_lds_sync();  // read before the next transform rewrites the image
+        }
+    }
+    __syncthreads();  // both waves' pilots visible; the images are free
+    double2 chv[2];
+    if (chan_g) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {  // D <= 256 = 2 x 128
+            const int d = tid + 128 * u;
+            chv[u] = chan_g[d < D ? d : 0];
+        }
+    }
+    // phys_pilot_ampl = sum |pilot| / (P*S*pilot_ampl)   (Frame.cpp:76-80),
+    // summed by wave 0 in rx_kernel's lane order
+    if (w == 0) {
+        double acc = 0.0;
+        for (int i = lane; i < S * P; i += T) acc += hypot(L.pil[i].x, L.pil[i].y);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+        if (lane == 0) L.red[0] = acc;
+    }
+    __syncthreads();
+    const double phys = L.red[0] / ((double)(P * S) * a.pilot_ampl);
+    // out = (F/phys) / ((F[s,p]/phys) / (F[0,p]/phys)) = F * gain[s][j]   (Frame.cpp:82-93)
+    for (int i = tid; i < S * P; i += 128) {
+        const int j = i % P;
+        const double2 c0 = make_double2(L.pil[j].x / phys, L.pil[j].y / phys);
+        const double2 cs = make_double2(L.pil[i].x / phys, L.pil[i].y / phys);
+        const double2 coef = cdiv_exact(cs, c0);
+        const double2 g = cdiv_exact(make_double2(1.0, 0.0), coef);
+        L.gain[i] = make_double2(g.x / phys, g.y / phys);
+    }
+    if (chan_g) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+            if (tid + 128 * u < D) L.chl[tid + 128 * u] = chv[u];
+    }
+    __syncthreads();
+    auto emit = [&](int s, const double2 (&yw)[RX_DPT]) {
+        double2* cbase = a.constell ? a.constell + (f * S + s) * D : nullptr;
+#pragma unroll
+        for (int i = 0; i < RX_DPT; ++i) {
+            int d = lane + T * i, gi = s * P + (pk[i] >> 16);
+            asm volatile("" : "+v"(d), "+v"(gi));  // opaque: not hoisted and held
+            if (d < D) {
+                double2 o = cmul_exact(yw[i], L.gain[gi]);
+                o = cmul_exact(o, L.chl[d]);  // main.cpp:69-71's divisor, as its reciprocal
+                if (cbase) store_nt(cbase + d, o);
+                dec[s * D + d] = (uint8_t)decide_select(o, a.k, s1, m);
+            }
+        }
+    };
+#pragma unroll
+    for (int q = 0; q < SH; ++q) {
+        const int s = 2 * q + w;
+        if (s < S) emit(s, y[q]);  // uniform
+    }
+    __syncthreads();  // decisions visible
+    if (a.bytes) {
+        if (by_word) {
+            const int per_word = 32 / a.k;  // decisions per output word
+            for (long wd = tid; wd < bpf / 4; wd += 128) {
+                const uint8_t* dw = dec + wd * per_word;
+                uint32_t word;
+                switch (a.k) {
+                    case 1: word = pack_word<1>(dw); break;
+                    case 2: word = pack_word<2>(dw); break;
+                    case 4: word = pack_word<4>(dw); break;
+                    default: word = pack_word<8>(dw); break;
+                }
+                reinterpret_cast<uint32_t*>(a.bytes + f * bpf)[wd] = word;
+            }
+        } else {
+            for (long jb = tid; jb < bpf; jb += 128) {
+                int byte = 0;
+                for (int b = 0; b < 8; ++b) {
+                    const long bit = jb * 8 + b;
+                    const long g = bit / a.k;
+                    const int within = (int)(bit % a.k);
+                    byte = (byte << 1) | ((dec[g] >> (a.k - 1 - within)) & 1);
+                }
+                a.bytes[f * bpf + jb] = (uint8_t)byte;
+            }
+        }
+    }
+    __syncthreads();  // dec / pil / gain / chl are rewritten by the next frame
+}
+
+}  // namespace ofdm

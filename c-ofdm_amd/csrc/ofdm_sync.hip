@@ -25,8 +25,10 @@
 #include <climits>
 #include <cstdint>
 
+#include "ofdm_dev.hpp"
 #include "ofdm_fft.hpp"
 #include "ofdm_fft32.hpp"
+#include "ofdm_rx2.hpp"
 #include "ofdm_sync.hpp"
 
 // The sync chain mirrors the reference's x86-64 arithmetic (no FMA): no
@@ -1052,28 +1054,52 @@ hipError_t launch_stream_params(int logn, const StreamParamsArgs& a, hipStream_t
 // replaces (same transforms, same reduction orders), so the results are the
 // same to the last bit.
 // ========================================================================
-__global__ void __launch_bounds__(128, 4) stream_sync_kernel(CfoArgs c, StreamParamsArgs a)
+// LDS of the sync stage (stream_sync_kernel, stream_decode_kernel).
+struct SyncLds {
+    double2* tw9;   // TwLds<9>
+    double2* tw7;   // TwLds<7>
+    double2* img;   // 640: the CFO transforms (amp over them), then the body FFT (512)
+    double2* pil;   // P
+    double2* dat;   // D/2 + 1 raw bins of the preamble (not over img[0, 512))
+    double2* red;   // 32
+    double2* cps;   // 1 + S raw CP sums
+    double* amp;    // 640 magnitudes (fftshifted), over img
+    double* ph;     // D/2 + 2
+    double* phi;    // 64 symbol phases
+    double* psi;    // 64 prefix sums
+    double* scal;   // cfo, phr, b, aa
+    int* wsum;      // P + 1 window maxima
+};
+
+// One located frame's sync stage (128 threads): writes cfo_out[f], the D
+// channel reciprocals to chan and the S ramps {A, B, cos(B*T), sin(B*T)} to
+// corr (global or LDS); returns after a barrier. load_tw: fill the twiddle
+// tables here (else they are resident and visible).
+__device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsArgs& a, long f, const SyncLds& Ls,
+                                           double2* chan, double* corr, bool load_tw)
 {
     // the geometry is fixed (host-checked): N = 512, cp = 128, L = 640 = 10 T
     constexpr int LOGN = 9, N = 512, T = 64, LOGM = 7, M = 128, G = 5, S5 = G * M, CP = 128, L = N + CP;
     constexpr int LT = L / T, CT = CP / T, RMAX = LT;
-    extern __shared__ double2 smem[];
-    double2* tw9 = smem;                                    // TwLds<9>
-    double2* tw7 = tw9 + TwLds<LOGN>::SIZE;                 // TwLds<7>
-    double2* img = tw7 + TwLds<LOGM>::SIZE;                 // G * M: the CFO transforms, then the body FFT
-    double2* pil = img + S5;                                // P
-    double2* dat = pil + a.P;                               // D/2 raw bins of the preamble
-    double2* red = dat + (a.D / 2 + 1);                     // 32
-    double2* cps = red + 32;                                // 1 + S raw CP sums
-    double* amp = reinterpret_cast<double*>(img);           // S5 magnitudes (fftshifted), over the transforms
-    double* ph = reinterpret_cast<double*>(cps + 1 + a.S);  // D/2 + 2
-    double* phi = ph + a.D / 2 + 2;                         // 64 symbol phases
-    double* psi = phi + 64;                                 // 64 prefix sums
-    double* scal = psi + 64;                                // cfo, phr, b, aa
-    int* wsum = reinterpret_cast<int*>(scal + 4);           // P + 1 window maxima
-    const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    const long f = blockIdx.x;
-    if (a.count && f >= *a.count) return;  // uniform: past the speculative frame count
+    double2* tw9 = Ls.tw9;
+    double2* tw7 = Ls.tw7;
+    double2* img = Ls.img;
+    double2* pil = Ls.pil;
+    double2* dat = Ls.dat;
+    double2* red = Ls.red;
+    double2* cps = Ls.cps;
+    double* amp = Ls.amp;
+    double* ph = Ls.ph;
+    double* phi = Ls.phi;
+    double* psi = Ls.psi;
+    double* scal = Ls.scal;
+    int* wsum = Ls.wsum;
+    // opaque per-frame copy of the thread index: the per-lane table loads and
+    // addresses are made here, not hoisted out of a caller's frame loop and
+    // held live across it
+    int tid;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"((int)threadIdx.x));
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const long x0 = a.starts[f];
     const int half = a.D / 2, Q = 1 + a.S;
     // ---------------------------------------------------------- pilot_freq_sinh (both waves)
@@ -1092,9 +1118,11 @@ __global__ void __launch_bounds__(128, 4) stream_sync_kernel(CfoArgs c, StreamPa
                 v[i] = c.x[j];
             }
         }
-        load_twiddles<LOGM>(c.tw_sub, tw7, tid, 128);
-        load_twiddles<LOGN>(a.tab.tw, tw9, tid, 128);
-        __syncthreads();  // twiddles visible
+        if (load_tw) {
+            load_twiddles<LOGM>(c.tw_sub, tw7, tid, 128);
+            load_twiddles<LOGN>(a.tab.tw, tw9, tid, 128);
+        }
+        __syncthreads();  // twiddles visible; the previous frame's LDS use is over
         if (w == 0 || lane < 16) fft_block_wave<LOGM, -1>(v, tt, tw7, img + g * M);
         __syncthreads();  // the five transforms visible
     }
@@ -1338,7 +1366,6 @@ __global__ void __launch_bounds__(128, 4) stream_sync_kernel(CfoArgs c, StreamPa
         }
     }
     // chan_char_lq's line, as reciprocals for the rx multiply
-    double2* chan = a.chan_out + f * a.D;
     for (int i = tid; i < a.D; i += 128) {
         double th;
         if (i < half)
@@ -1357,21 +1384,135 @@ __global__ void __launch_bounds__(128, 4) stream_sync_kernel(CfoArgs c, StreamPa
         const double B = -2.0 * M_PI * cfo - phi[q] / N;
         double sn, cs;
         sincos(B * T, &sn, &cs);
-        double* o = a.corr_out + (f * a.S + s) * 4;
+        double* o = corr + s * 4;
         o[0] = A;
         o[1] = B;
         o[2] = cs;
         o[3] = sn;
     }
+    __syncthreads();  // the outputs visible (LDS); the stage's LDS is free
+}
+
+__global__ void __launch_bounds__(128, 4) stream_sync_kernel(CfoArgs c, StreamParamsArgs a)
+{
+    extern __shared__ double2 smem[];
+    SyncLds Ls;
+    Ls.tw9 = smem;
+    Ls.tw7 = Ls.tw9 + TwLds<9>::SIZE;
+    Ls.img = Ls.tw7 + TwLds<7>::SIZE;
+    Ls.pil = Ls.img + 640;
+    Ls.dat = Ls.pil + a.P;
+    Ls.red = Ls.dat + (a.D / 2 + 1);
+    Ls.cps = Ls.red + 32;
+    Ls.amp = reinterpret_cast<double*>(Ls.img);
+    Ls.ph = reinterpret_cast<double*>(Ls.cps + 1 + a.S);
+    Ls.phi = Ls.ph + a.D / 2 + 2;
+    Ls.psi = Ls.phi + 64;
+    Ls.scal = Ls.psi + 64;
+    Ls.wsum = reinterpret_cast<int*>(Ls.scal + 4);
+    const long f = blockIdx.x;
+    if (a.count && f >= *a.count) return;  // uniform: past the speculative frame count
+    sync_frame(c, a, f, Ls, a.chan_out + f * a.D, a.corr_out + f * a.S * 4, true);
+}
+
+// ========================================================================
+// The whole fused stream decode in one kernel (N = 512, 640-point CFO form):
+// one workgroup per located frame runs sync_frame (pilot_freq_sinh, the CP / phase
+// corrections, chan_char_lq; Frame.hpp:238-348,389-434) and then rx2_frame
+// (the 8 message transforms, equalisation, channel, decisions;
+// Frame.cpp:73-96, main.cpp:67-71, modulation.cpp:53-87) in the same
+// two-wave workgroup, the ramps and the channel passed through LDS. Each
+// frame's samples are read once from HBM (the preamble, then the CP pairs,
+// then the bodies, whose CP-pair tails are fresh in the caches), and the
+// latency-bound sync stage of one frame overlaps the bandwidth-bound
+// transforms of the CU's other frames. LDS (~19.4 KB: 8 frames per CU at 4
+// waves per SIMD): the 512-point twiddles, one 16 KB region (the sync stage's
+// transforms and 128-point twiddles, then the two rx images, then the
+// decisions and the channel), the ramps, and the two stages' small arrays
+// over each other. The channel reciprocals go through the chan scratch (L2)
+// from the sync stage to the rx stage's emit.
+// ========================================================================
+template <bool I16>
+__global__ void __launch_bounds__(128, 4) stream_decode_kernel(CfoArgs c, StreamParamsArgs a, RxArgs r)
+{
+    extern __shared__ double2 smem[];
+    const int S = a.S, D = a.D, P = a.P;
+    double2* tw9 = smem;
+    double2* A = tw9 + TwLds<9>::SIZE;        // 1024: sync transforms (+ tw7) / dat / ph, then the rx images
+    double2* tw7 = A + 640;                   // over A, past the CFO transforms (dead with them)
+    double* corr = reinterpret_cast<double*>(A + 1024);  // S*4 ramps
+    double2* U = reinterpret_cast<double2*>(corr + 4 * S);  // the stages' small arrays, over each other
+    SyncLds Ls;
+    Ls.tw9 = tw9;
+    Ls.tw7 = tw7;
+    Ls.img = A;
+    Ls.amp = reinterpret_cast<double*>(A);
+    Ls.dat = A + 512;
+    Ls.ph = reinterpret_cast<double*>(A + 650);
+    Ls.pil = U;
+    Ls.red = Ls.pil + P;
+    Ls.cps = Ls.red + 32;
+    Ls.phi = reinterpret_cast<double*>(Ls.cps + 1 + S);
+    Ls.psi = Ls.phi + 64;
+    Ls.scal = Ls.psi + 64;
+    Ls.wsum = reinterpret_cast<int*>(Ls.scal + 4);
+    Rx2Lds Lr;
+    Lr.img = A;
+    Lr.tw = tw9;
+    Lr.pil = U;
+    Lr.gain = U + S * P;
+    Lr.chl = A + ((S * D + 15) >> 4);  // over the images, past the decisions (rx2_frame stages it)
+    Lr.red = reinterpret_cast<double*>(Lr.gain + S * P);
+    const int lane0 = threadIdx.x & 63;
+    const long f = blockIdx.x;
+    if (a.count && f >= *a.count) return;  // uniform: past the speculative frame count
+    // one frame per workgroup (a persistent frame loop let the compiler hoist
+    // the sync stage's math-library constants and tables out of it: spills)
+    int pk[RX_DPT];
+#pragma unroll
+    for (int i = 0; i < RX_DPT; ++i) pk[i] = r.tab.rx_pack[lane0 + 64 * i];
+    const int pbin = r.tab.pilot_swz[lane0];
+    double2* chan = a.chan_out + f * D;
+    sync_frame(c, a, f, Ls, chan, corr, true);
+    rx2_frame<I16>(r, f, Lr, corr, pk, pbin, chan);
+}
+
+static bool stream_sync_geometry(const CfoArgs& c, const StreamParamsArgs& a, int logn, int logm, int g)
+{
+    const int L = (1 << logn) + a.cp;
+    return logn == 9 && logm == 7 && g == 5 && L == 640 && a.npr == 1 && a.S + 1 <= 64 && a.S <= RX_SMAX &&
+           a.cp == 128 && a.D <= 256 && a.P <= 64 && c.P == a.P;
+}
+
+template <bool I16>
+static hipError_t decode_launch(const CfoArgs& c, const StreamParamsArgs& a, const RxArgs& r, hipStream_t st)
+{
+    const size_t shm = sizeof(double2) * (TwLds<9>::SIZE + 1024) + sizeof(double) * 4 * a.S +
+                       std::max(sizeof(double2) * (2 * (size_t)a.S * a.P) + sizeof(double) * 2,
+                                sizeof(double2) * (a.P + 32 + 1 + a.S) + sizeof(double) * 132 + sizeof(int) * (a.P + 2));
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)stream_decode_kernel<I16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL(stream_decode_kernel<I16>, dim3((unsigned)a.nframes), dim3(128), shm, st, c, a, r);
+    return hipGetLastError();
+}
+
+hipError_t launch_stream_decode(const CfoArgs& c, const StreamParamsArgs& a, const RxArgs& r, int logn, int logm, int g,
+                                hipStream_t st)
+{
+    if (a.nframes <= 0) return hipSuccess;
+    if (!stream_sync_geometry(c, a, logn, logm, g) || !r.chan_recip || r.D != a.D || r.S != a.S || r.P != a.P)
+        return hipErrorNotSupported;  // the staged launches cover other geometries
+    return r.iq16 ? decode_launch<true>(c, a, r, st) : decode_launch<false>(c, a, r, st);
 }
 
 hipError_t launch_stream_sync(const CfoArgs& c, const StreamParamsArgs& a, int logn, int logm, int g, hipStream_t st)
 {
     if (a.nframes <= 0) return hipSuccess;
-    const int L = (1 << logn) + a.cp;
-    if (logn != 9 || logm != 7 || g != 5 || L != 640 || a.npr != 1 || a.S + 1 > 64 || a.cp != 128 ||
-        a.D > 256 || a.P > 64 || c.P != a.P)
-        return hipErrorNotSupported;  // the two-kernel path covers other geometries
+    if (!stream_sync_geometry(c, a, logn, logm, g)) return hipErrorNotSupported;  // the two-kernel path covers other geometries
     const size_t shm = sizeof(double2) * (TwLds<9>::SIZE + TwLds<7>::SIZE + 640 + a.P + (a.D / 2 + 1) + 32 + 1 + a.S) +
                        sizeof(double) * (a.D / 2 + 2 + 64 + 64 + 4) + sizeof(int) * (a.P + 2);
     static bool attr = false;

@@ -166,6 +166,10 @@ hipError_t launch_stream_params(int logn, const StreamParamsArgs& a, hipStream_t
 // pilot_freq_sinh + the params stage fused (N = 512, 640-point CFO form);
 // hipErrorNotSupported for other geometries (use launch_cfo + launch_stream_params)
 hipError_t launch_stream_sync(const CfoArgs& c, const StreamParamsArgs& a, int logn, int logm, int g, hipStream_t st);
+// the whole fused decode (sync stage + rx stage) in one kernel for the same
+// geometries (r: the stream rx arguments; corr / chan pass through LDS)
+hipError_t launch_stream_decode(const CfoArgs& c, const StreamParamsArgs& a, const RxArgs& r, int logn, int logm, int g,
+                                hipStream_t st);
 
 hipError_t launch_stream_walk(int logt, const WalkArgs& a, long nblocks, hipStream_t st);
 // stream walkers resident at once on the current device (occupancy of the
