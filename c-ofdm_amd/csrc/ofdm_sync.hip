@@ -2368,59 +2368,74 @@ hipError_t launch_stream_walk(int logt, const WalkArgs& a, long nblocks, hipStre
     }
 }
 
-// One workgroup: blocks of 1024 chunks; an exclusive scan of their in-core
-// record counts, then the block's records are copied in parallel.
+// One workgroup: blocks of 1024 x CPT chunks (CPT consecutive chunks per
+// thread; 2048 chunks are one block): an exclusive scan of their in-core
+// record counts, then each output slot finds its chunk by binary search over
+// the scan, each thread gathering G records before storing any (so the
+// loads overlap).
 __global__ void __launch_bounds__(1024) compact_kernel(CompactArgs a)
 {
-    constexpr int G = 16;
-    __shared__ long excl[1024];  // exclusive scan of the block's counts
-    __shared__ long srcb[1024];  // rec index of each chunk's first in-core record
+    constexpr int CPT = 4, G = 16, NB = 1024 * CPT;
+    __shared__ int excl[NB];  // exclusive scan of the block's counts
+    __shared__ int srcb[NB];  // rec index of each chunk's first in-core record
     __shared__ long wsum[16];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const long* __restrict__ rec = a.rec;
     long base = 0;
-    for (long k0 = 0; k0 < a.nchunks; k0 += 1024) {
-        const long k = k0 + t;
+    for (long k0 = 0; k0 < a.nchunks; k0 += NB) {
         // only stored records: an overflowing walk (nrec > max_rec) kept the
         // first max_rec, the host rejects it, and nothing past them is read
-        long cnt = 0, src = 0;  // src: rec index of the chunk's first in-core record
-        if (k < a.nchunks) {
-            const int fi = a.first_in[k];
-            cnt = max(0, min(a.ncore[k], a.max_rec - fi));
-            src = k * a.max_rec + fi;
+        int cnt[CPT], mine = 0;
+#pragma unroll
+        for (int u = 0; u < CPT; ++u) {
+            const long k = k0 + (long)t * CPT + u;
+            cnt[u] = 0;
+            int src = 0;
+            if (k < a.nchunks) {
+                const int fi = a.first_in[k];
+                cnt[u] = max(0, min(a.ncore[k], a.max_rec - fi));
+                src = (int)(k * a.max_rec + fi);
+            }
+            srcb[t * CPT + u] = src;
+            mine += cnt[u];
         }
-        long inc = cnt;  // inclusive scan: wave, then wave totals
+        int inc = mine;  // inclusive scan: wave, then wave totals
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
-            const long y = __shfl_up(inc, o);
+            const int y = __shfl_up(inc, o);
             if (lane >= o) inc += y;
         }
         if (lane == 63) wsum[w] = inc;
         __syncthreads();
-        long off = inc - cnt;
-        for (int u = 0; u < w; ++u) off += wsum[u];
+        int off = inc - mine;
+        for (int u = 0; u < w; ++u) off += (int)wsum[u];
         long tot = 0;
         for (int u = 0; u < 16; ++u) tot += wsum[u];
-        excl[t] = off;
-        srcb[t] = src;
+#pragma unroll
+        for (int u = 0; u < CPT; ++u) {
+            excl[t * CPT + u] = off;
+            off += cnt[u];
+        }
         __syncthreads();
-        // output slot -> chunk by binary search over the scan; each thread
-        // gathers G records before storing any, so the loads overlap
-        const int nb = (int)min(1024L, a.nchunks - k0);
+        const int nb = (int)min((long)NB, a.nchunks - k0);
         for (long i0 = 0; i0 < tot; i0 += 1024 * G) {
             long pbv[G];
+            // branch-free (a load inside a per-slot branch waits before the
+            // next is issued): every slot searches and loads, clamped
 #pragma unroll
             for (int g = 0; g < G; ++g) {
-                const long idx = i0 + g * 1024 + t;
-                pbv[g] = 0;
-                if (idx < tot) {
-                    int lo = 0, hi = nb;  // last j with excl[j] <= idx
-                    while (hi - lo > 1) {
-                        const int mid = (lo + hi) >> 1;
-                        if (excl[mid] <= idx) lo = mid; else hi = mid;
-                    }
-                    pbv[g] = rec[srcb[lo] + (idx - excl[lo])];
+                const long idx0 = i0 + g * 1024 + t;
+                const int idx = (int)(idx0 < tot ? idx0 : tot - 1);
+                int lo = 0, hi = nb;  // last j with excl[j] <= idx
+#pragma unroll
+                for (int it = 0; it < 13; ++it) {  // nb <= 4096 = 2^12: 13 halvings reach hi - lo == 1
+                    const int mid = (lo + hi) >> 1;
+                    const bool go = hi - lo > 1;
+                    const bool le = excl[mid] <= idx;
+                    lo = go && le ? mid : lo;
+                    hi = go && !le ? mid : hi;
                 }
+                pbv[g] = rec[srcb[lo] + (idx - excl[lo])];
             }
 #pragma unroll
             for (int g = 0; g < G; ++g) {
