@@ -2153,7 +2153,7 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
                 // of the FP32 transform and sums) decide as FP64
                 // does; when the first block that is not a certain FAIL is
                 // uncertain, the step is evaluated again in FP64.
-                float2* fftb32 = reinterpret_cast<float2*>(big);
+                float4* fftb32 = reinterpret_cast<float4*>(big);  // one image per group, both blocks
                 const float lev = (float)a.t2_level, marg = (float)a.t2_margin;
                 for (long base = pos;; base += 2L * G * N) {
                     WPROF(++p_n2;)
@@ -2165,18 +2165,22 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
                     asm volatile("v_mov_b32 %0, %1" : "=v"(tt) : "v"(tt0));
                     const long bA = base + (long)g * N, bB = bA + (long)G * N;
                     const bool liveA = bA + N <= a.n, liveB = bB + N <= a.n;
-                    float2 va[8], vb[8];
-                    load8_block32<T>(a, bA + tt, liveA, va);
-                    load8_block32<T>(a, bB + tt, liveB, vb);
-                    fft_regs_wave32<LOGT, -1>(va, tt, lds_tw, fftb32 + g * N);
-                    fft_regs_wave32<LOGT, -1>(vb, tt, lds_tw, fftb32 + (g + G) * N);
+                    float4 v[8];
+                    {
+                        float2 va[8], vb[8];
+                        load8_block32<T>(a, bA + tt, liveA, va);
+                        load8_block32<T>(a, bB + tt, liveB, vb);
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) v[i] = make_float4(va[i].x, va[i].y, vb[i].x, vb[i].y);
+                    }
+                    fft_regs_wave32x2<LOGT, -1>(v, tt, lds_tw, fftb32 + g * N);
                     float ta = 0.f, sa = 0.f, tb = 0.f, sb = 0.f;
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {
                         const int k = tt + T * i;
                         const float m = (float)((k >= a.a1 && k <= a.b1) + (k >= a.a2 && k <= a.b2));
-                        const float ea = va[i].x * va[i].x + va[i].y * va[i].y;
-                        const float eb = vb[i].x * vb[i].x + vb[i].y * vb[i].y;
+                        const float ea = v[i].x * v[i].x + v[i].y * v[i].y;
+                        const float eb = v[i].z * v[i].z + v[i].w * v[i].w;
                         ta += ea;
                         sa += m * ea;
                         tb += eb;
