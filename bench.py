@@ -264,6 +264,86 @@ def stream_leg(args, dist, dev, world, rank, M, i16: bool):
     return res
 
 
+CONFIG_C = dict(CONFIG_B, fft_size=4096, num_data_subc=2048, num_pilot_subc=64, cp_size=1024, mod_type=4)
+
+
+def config3_leg(args, dist, dev, world, rank, M):
+    """SURVEY §8d config 3 (BASELINE configs[2]): config C (N=4096, D=2048,
+    P=64, cp=1024, 16-QAM, 8 symbols per frame). (1) The loopback step
+    timed as the headline one (tx with fused AWGN at Es/N0 = 10 dB, then rx
+    with constellation, bytes and bit errors; frames per GPU, weak scaling);
+    (2) the AWGN BER sweep, Es/N0 0..30 dB step 2, >= 1e7 bits per point per
+    GPU, seed 1000 + SNR (tools/ber_sweep.py's definition), errors and bits
+    summed over the ranks."""
+    import torch
+    import ofdm_dist
+    p = dict(CONFIG_C)
+    modem = M.Modem(p, dev.index)
+    geo = modem.geo
+    nf, S = args.config3_frames, p["num_symb"]
+    msg, bpf = geo.message_len, geo.bytes_per_frame
+    f0 = rank * nf
+    data = torch.from_numpy(payload_bytes(f0 * bpf, nf * bpf)).to(dev)
+    iq = torch.empty((nf * msg,), dtype=torch.complex128, device=dev)
+    cons = torch.empty((nf * p["num_data_subc"] * S,), dtype=torch.complex128, device=dev)
+    out = torch.empty_like(data)
+    errs = torch.zeros((1,), dtype=torch.int64, device=dev)
+    es = 10.0 / 9.0  # mean energy of the reference's 16-QAM table (modulation.cpp:4-36): levels +-1/3, +-1 per axis
+    stream = torch.cuda.current_stream(dev)
+
+    def std_for(db):
+        return float(np.sqrt(es / 10 ** (db / 10)))
+
+    def step(events=None):
+        if events:
+            events[0].record(stream)
+        modem.tx(data, nf, iq, noise_std=std_for(10.0), seed=1010, sample_offset=f0 * msg, stream=stream)
+        if events:
+            events[1].record(stream)
+        modem.rx(iq, nf, constell_out=cons, bytes_out=out, ref=data, bit_errors=errs, stream=stream)
+        if events:
+            events[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    ev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(ev[i])
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    elapsed = ofdm_dist.max_over_ranks(time.perf_counter() - t0, dev, dist)
+    tx_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+    rx_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+    rx_bytes = nf * S * rx_bytes_per_symbol(p)
+    # BER sweep on a prefix of the frames (>= 1e7 bits per point per GPU)
+    nb = min(nf, int(np.ceil(1e7 / (8 * bpf))))
+    rows = []
+    for db in range(0, 31, 2):
+        errs.zero_()
+        modem.tx(data, nb, iq, noise_std=std_for(db), seed=1000 + db, sample_offset=f0 * msg, stream=stream)
+        modem.rx(iq, nb, bytes_out=out, ref=data, bit_errors=errs, stream=stream)
+        cnt = torch.cat([errs, torch.tensor([8 * nb * bpf], dtype=torch.int64, device=dev)])
+        ofdm_dist.reduce_counters(cnt, dist)
+        e, b = (int(v) for v in cnt.cpu().numpy())
+        rows.append({"es_n0_db": db, "bits": b, "bit_errors": e, "ber": e / b})
+    modem.close()
+    return {"metric": "IQ-samples/sec (tx IFFT+CP and rx FFT+equalise), config C 4096-subcarrier 16-QAM frames",
+            "workload": f"config3_C_N4096_D2048_P64_cp1024_16QAM_{nf}frames_x8sym_per_gpu",
+            "value": world * args.steps * nf * msg / elapsed, "unit": "IQ-samples/s", "n_gpus": world,
+            "scaling": "weak", "steps": args.steps, "ms_per_step": elapsed / args.steps * 1e3, "dtype": "f64",
+            "tx_avg_launch_ms": tx_ms, "rx_avg_launch_ms": rx_ms,
+            "roofline": {"bound": "hbm", "kernel": "rx (CP strip+FFT+equalise+demap), config C",
+                         "achieved": rx_bytes / (rx_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": rx_bytes / (rx_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "algorithmic_bytes_per_launch": rx_bytes, "avg_launch_ms": rx_ms},
+            "ber_sweep": {"es_n0_db": "0..30 step 2", "seed": "1000 + Es/N0", "frames_per_gpu": nb, "points": rows}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
@@ -286,6 +366,8 @@ def main():
     ap.add_argument("--stream-reps", type=int, default=10)
     ap.add_argument("--stream-warmup", type=int, default=3)
     ap.add_argument("--stream-cpu-budget", type=float, default=8.0)
+    ap.add_argument("--no-config3", action="store_true", help="skip the config-3 (config C) sub-record")
+    ap.add_argument("--config3-frames", type=int, default=4096, help="config C frames per GPU (weak)")
     args = ap.parse_args()
 
     import ofdm_dist
@@ -430,6 +512,9 @@ def main():
         torch.cuda.empty_cache()
         result["stream"] = stream_leg(args, dist, dev, world, rank, M, i16=False)
         result["stream_int16"] = stream_leg(args, dist, dev, world, rank, M, i16=True)
+    if not args.no_config3:
+        torch.cuda.empty_cache()
+        result["config3"] = config3_leg(args, dist, dev, world, rank, M)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:

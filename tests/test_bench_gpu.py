@@ -26,7 +26,7 @@ def _bench(*argv, timeout=240):
 
 
 def test_bench_two_ranks_equal_one_rank_over_the_same_frames():
-    common = ["--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-stream"]
+    common = ["--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-stream", "--no-config3"]
     one = _bench("--frames", "128", *common)
     two = _bench("--gpus", "2", "--backend", "gloo", "--frames", "64", *common)
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2
@@ -37,9 +37,24 @@ def test_bench_two_ranks_equal_one_rank_over_the_same_frames():
 
 
 def test_bench_strong_scaling_shards_total_frames():
-    common = ["--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-stream"]
+    common = ["--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-stream", "--no-config3"]
     one = _bench("--total-frames", "101", *common)
     three = _bench("--gpus", "3", "--backend", "gloo", "--total-frames", "101", *common)
     assert three["scaling"] == "strong" and three["n_gpus"] == 3
     assert three["frames"] == one["frames"] == 101
     assert three["bit_errors"] == one["bit_errors"]
+
+
+def test_bench_config3_record():
+    # SURVEY §8d config 3 in the driver's bench line: the config-C loopback
+    # step and the AWGN BER sweep (0..30 dB, >= 1e7 bits per point)
+    r = _bench("--steps", "2", "--warmup", "1", "--frames", "64", "--no-cpu-baseline", "--no-stream",
+               "--config3-frames", "160")
+    c3 = r["config3"]
+    assert c3["n_gpus"] == 1 and c3["value"] > 0 and 0 < c3["roofline"]["frac"] < 1
+    pts = c3["ber_sweep"]["points"]
+    assert [p["es_n0_db"] for p in pts] == list(range(0, 31, 2))
+    assert all(p["bits"] >= 10_000_000 for p in pts)
+    bers = [p["ber"] for p in pts]
+    assert 0.25 < bers[0] < 0.4 and bers[-1] == 0.0  # 16-QAM: ~1/3 at 0 dB, error-free at 30 dB
+    assert all(b1 <= b0 + 1e-3 for b0, b1 in zip(bers, bers[1:]))
