@@ -248,13 +248,16 @@ def stream_leg(args, dist, dev, world, rank, M, i16: bool):
            "stream_GB": layout.n * esz / 1e9, "frames_sent": layout.total_frames, "frames_found": int(tot[0]),
            "frames_error_free": int(tot[1]), "rewalks_per_call": int(tot[2]) / args.stream_reps,
            "halo": rx.halo, "tail": rx.tail,
-           "roofline": {"bound": "hbm", "kernel": "whole stream pipeline (walker + compaction + cfo + params + "
-                                                  "stream rx, host stitching overlapped)",
+           "roofline": {"bound": "hbm", "kernel": "whole stream pipeline (walker + compaction + fused decode, "
+                                                  "host stitching overlapped)",
                         "achieved": alg_rank / (call_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": alg_rank / (call_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                         "algorithmic_bytes_per_call": alg_rank, "avg_call_ms": call_ms,
                         "traffic": (pmc or {}).get("hbm_bytes_per_call")},
            "cpu_baseline": None}
+    if world == 1 and args.stream_pipeline > 1:
+        res["pipelined"] = stream_pipelined(args, p, M, dev, modem, layout, rx, walk, outs, x, nsl, cap, i16,
+                                            n_owned, exchange, SS)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not i16:
         try:
             res["cpu_baseline"] = cpu_stream_baseline(p, x[:1 << 27].cpu().numpy(), args.stream_cpu_budget)
@@ -262,6 +265,48 @@ def stream_leg(args, dist, dev, world, rank, M, i16: bool):
             res["cpu_baseline"] = {"error": repr(e)}
     modem.close()
     return res
+
+
+def stream_pipelined(args, p, M, dev, modem, layout, rx, walk, outs, x, nsl, cap, i16, n_owned, exchange, SS):
+    """The same stream received by `stream_pipeline` contexts in turn, each on
+    its own HIP stream with its own outputs (double-buffered receive): call
+    k + 1's walk runs while call k's decode drains. Throughput of back-to-back
+    calls (one timed region); every context's outputs are checked against the
+    serial calls'."""
+    import torch
+    P = args.stream_pipeline
+    mods, sts, walks, rxs, outl = [modem], [torch.cuda.current_stream(dev)], [walk], [rx], [outs]
+    for _ in range(P - 1):
+        m2 = M.Modem(p, dev.index)
+        st2 = torch.cuda.Stream(dev)
+        o2 = {k: torch.empty_like(v) for k, v in outs.items()}
+        r2 = SS.ShardedStreamRx(p, layout.n, 1, 0)
+        mods.append(m2)
+        sts.append(st2)
+        outl.append(o2)
+        rxs.append(r2)
+        walks.append(SS.hip_walker(m2, x, nsl, r2.own_lo - r2.slice_lo, r2.own_hi - r2.slice_lo, cap, o2, i16=i16,
+                                   stream=st2))
+    for i in range(P):
+        rxs[i].run(walks[i], exchange)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.stream_reps * P):
+        rxs[k % P].run(walks[k % P], exchange)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    same = all(r.n_owned == n_owned for r in rxs[1:])
+    k = min(n_owned, cap)
+    for o in outl[1:]:
+        same = same and bool(torch.equal(o["pb_out"][:k], outs["pb_out"][:k])) and \
+            bool(torch.equal(o["bytes_out"][:k * layout.bpf], outs["bytes_out"][:k * layout.bpf]))
+    for m2 in mods[1:]:
+        m2.close()
+    return {"contexts": P, "value": layout.n * args.stream_reps * P / el, "unit": "stream samples/s",
+            "ms_per_call": el / (args.stream_reps * P) * 1e3, "calls": args.stream_reps * P,
+            "outputs_match_serial": same,
+            "note": "back-to-back calls on the same stream, alternating contexts/HIP streams (call k+1's walk "
+                    "overlaps call k's decode); the record's value is the serial per-call figure"}
 
 
 CONFIG_C = dict(CONFIG_B, fft_size=4096, num_data_subc=2048, num_pilot_subc=64, cp_size=1024, mod_type=4)
@@ -366,6 +411,8 @@ def main():
     ap.add_argument("--stream-reps", type=int, default=10)
     ap.add_argument("--stream-warmup", type=int, default=3)
     ap.add_argument("--stream-cpu-budget", type=float, default=8.0)
+    ap.add_argument("--stream-pipeline", type=int, default=2,
+                    help="contexts for the stream record's pipelined figure (1: off; one GPU only)")
     ap.add_argument("--no-config3", action="store_true", help="skip the config-3 (config C) sub-record")
     ap.add_argument("--config3-frames", type=int, default=4096, help="config C frames per GPU (weak)")
     args = ap.parse_args()

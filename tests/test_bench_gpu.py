@@ -58,3 +58,17 @@ def test_bench_config3_record():
     bers = [p["ber"] for p in pts]
     assert 0.25 < bers[0] < 0.4 and bers[-1] == 0.0  # 16-QAM: ~1/3 at 0 dB, error-free at 30 dB
     assert all(b1 <= b0 + 1e-3 for b0, b1 in zip(bers, bers[1:]))
+
+
+def test_bench_stream_record_with_pipelined_figure():
+    # SURVEY §8d config 4 in the driver's bench line (small stream): the serial
+    # per-call record, and the two-context pipelined figure whose outputs equal
+    # the serial calls'
+    r = _bench("--steps", "1", "--warmup", "1", "--frames", "64", "--no-cpu-baseline", "--no-config3",
+               "--stream-frames", "512", "--stream-reps", "2", "--stream-warmup", "1")
+    for key in ("stream", "stream_int16"):
+        s = r[key]
+        assert s["value"] > 0 and s["frames_found"] >= 0.95 * s["frames_sent"]
+        pp = s["pipelined"]
+        assert pp["contexts"] == 2 and pp["calls"] == 4 and pp["outputs_match_serial"] is True
+        assert pp["value"] > 0

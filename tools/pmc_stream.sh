@@ -15,7 +15,7 @@ for ctr, path in (("FETCH_SIZE", "gpurun_out/pmcs_fetch/run_counter_collection.c
     for r in csv.DictReader(open(path)):
         k = r["Kernel_Name"]
         for key in ("stream_walk_kernel", "compact_kernel", "cfo_kernel", "stream_params_kernel", "stream_sync_kernel",
-                    "rx_stream2_kernel", "rx_kernel"):
+                    "rx_stream2_kernel", "stream_decode_kernel", "rx_kernel"):
             if key in k and r["Counter_Name"] == ctr:
                 acc[(key, ctr)].append(float(r["Counter_Value"]))
 out = {"note": "KiB per dispatch (mean over the bench's dispatches: warm-up + 1 timed); "
