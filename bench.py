@@ -409,7 +409,7 @@ def main():
     ap.add_argument("--no-stream", action="store_true", help="skip the config-4 stream sub-record")
     ap.add_argument("--stream-frames", type=int, default=16384, help="config-4 stream frames per GPU (weak)")
     ap.add_argument("--stream-reps", type=int, default=10)
-    ap.add_argument("--stream-warmup", type=int, default=3)
+    ap.add_argument("--stream-warmup", type=int, default=10, help="untimed stream calls (clocks ramp)")
     ap.add_argument("--stream-cpu-budget", type=float, default=8.0)
     ap.add_argument("--stream-pipeline", type=int, default=2,
                     help="contexts for the stream record's pipelined figure (1: off; one GPU only)")

@@ -2372,14 +2372,14 @@ hipError_t launch_stream_walk(int logt, const WalkArgs& a, long nblocks, hipStre
     }
 }
 
-// One workgroup: blocks of 1024 x CPT chunks (CPT consecutive chunks per
-// thread; 2048 chunks are one block): an exclusive scan of their in-core
-// record counts, then each output slot finds its chunk by binary search over
-// the scan, each thread gathering G records before storing any (so the
-// loads overlap).
+// Blocks of 1024 x CPT chunks (CPT consecutive chunks per thread; 2048
+// chunks are one block): every workgroup scans their in-core record counts
+// (exclusive), then each output slot finds its chunk by binary search over the
+// scan; the slots are spread over the workgroups (G per thread, gathered
+// before any is stored, so the loads overlap).
 __global__ void __launch_bounds__(1024) compact_kernel(CompactArgs a)
 {
-    constexpr int CPT = 4, G = 16, NB = 1024 * CPT;
+    constexpr int CPT = 4, G = 2, NB = 1024 * CPT;
     __shared__ int excl[NB];  // exclusive scan of the block's counts
     __shared__ int srcb[NB];  // rec index of each chunk's first in-core record
     __shared__ long wsum[16];
@@ -2389,18 +2389,21 @@ __global__ void __launch_bounds__(1024) compact_kernel(CompactArgs a)
     for (long k0 = 0; k0 < a.nchunks; k0 += NB) {
         // only stored records: an overflowing walk (nrec > max_rec) kept the
         // first max_rec, the host rejects it, and nothing past them is read
-        int cnt[CPT], mine = 0;
+        // branch-free: every thread loads its (clamped) chunks' counts
+        // together (loads under a per-chunk branch were waited one by one)
+        int cnt[CPT], fiv[CPT], ncv[CPT], mine = 0;
+#pragma unroll
+        for (int u = 0; u < CPT; ++u) {
+            const long k = min(k0 + (long)t * CPT + u, a.nchunks - 1);
+            fiv[u] = a.first_in[k];
+            ncv[u] = a.ncore[k];
+        }
 #pragma unroll
         for (int u = 0; u < CPT; ++u) {
             const long k = k0 + (long)t * CPT + u;
-            cnt[u] = 0;
-            int src = 0;
-            if (k < a.nchunks) {
-                const int fi = a.first_in[k];
-                cnt[u] = max(0, min(a.ncore[k], a.max_rec - fi));
-                src = (int)(k * a.max_rec + fi);
-            }
-            srcb[t * CPT + u] = src;
+            const bool in = k < a.nchunks;
+            cnt[u] = in ? max(0, min(ncv[u], a.max_rec - fiv[u])) : 0;
+            srcb[t * CPT + u] = in ? (int)(k * a.max_rec + fiv[u]) : 0;
             mine += cnt[u];
         }
         int inc = mine;  // inclusive scan: wave, then wave totals
@@ -2422,7 +2425,7 @@ __global__ void __launch_bounds__(1024) compact_kernel(CompactArgs a)
         }
         __syncthreads();
         const int nb = (int)min((long)NB, a.nchunks - k0);
-        for (long i0 = 0; i0 < tot; i0 += 1024 * G) {
+        for (long i0 = (long)blockIdx.x * 1024 * G; i0 < tot; i0 += (long)gridDim.x * 1024 * G) {
             long pbv[G];
             // branch-free (a load inside a per-slot branch waits before the
             // next is issued): every slot searches and loads, clamped
@@ -2453,7 +2456,7 @@ __global__ void __launch_bounds__(1024) compact_kernel(CompactArgs a)
         base += tot;
         __syncthreads();  // excl / srcb / wsum are rewritten by the next block
     }
-    if (t == 0) {
+    if (t == 0 && blockIdx.x == 0) {
         *a.count = base;
         if (a.queue_reset) *a.queue_reset = 0;
     }
@@ -2461,7 +2464,10 @@ __global__ void __launch_bounds__(1024) compact_kernel(CompactArgs a)
 
 hipError_t launch_compact(const CompactArgs& a, hipStream_t st)
 {
-    hipLaunchKernelGGL(compact_kernel, dim3(1), dim3(1024), 0, st, a);
+    // every block scans the counts; the output slots are spread over the
+    // blocks (one CU's LDS was the limit: 16 binary searches per thread there)
+    const long nb = std::max(1L, std::min(64L, (a.cap + 2047) / 2048));
+    hipLaunchKernelGGL(compact_kernel, dim3((unsigned)nb), dim3(1024), 0, st, a);
     return hipGetLastError();
 }
 
