@@ -142,8 +142,10 @@ __device__ __forceinline__ void rx2_frame(const RxArgs& a, long f, const Rx2Lds&
         const double2 c0 = make_double2(L.pil[j].x / phys, L.pil[j].y / phys);
         const double2 cs = make_double2(L.pil[i].x / phys, L.pil[i].y / phys);
         const double2 coef = cdiv_exact(cs, c0);
-        const double2 g = cdiv_exact(make_double2(1.0, 0.0), coef);
-        L.gain[i] = make_double2(g.x / phys, g.y / phys);
+        // the divisor's reciprocal as conj / |.|^2 (the points are multiplied,
+        // not divided as the reference does: within rounding either way)
+        const double r = 1.0 / (coef.x * coef.x + coef.y * coef.y);
+        L.gain[i] = make_double2(coef.x * r / phys, -coef.y * r / phys);
     }
     if (chan_g) {
 #pragma unroll

@@ -1374,7 +1374,11 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
             th = add_rn(add_rn(mul_rn(-b, (double)a.D) / 2, mul_rn((double)(i - half), b)), aa);
         double sn, cs;
         sincos(th, &sn, &cs);
-        chan[i] = a.chan_recip ? cdiv_exact(make_double2(1.0, 0.0), make_double2(cs, sn)) : make_double2(cs, sn);
+        // the reciprocal of the unit phasor as conj / |.|^2 (one division; within
+        // 2 ulp of the exactly rounded quotient, which rx's multiply does not
+        // reproduce anyway: the reference divides each point)
+        const double r = 1.0 / (cs * cs + sn * sn);
+        chan[i] = a.chan_recip ? make_double2(cs * r, -sn * r) : make_double2(cs, sn);
     }
     __syncthreads();  // psi visible
     // message symbols: theta(m) = A_s + B_s m over the CP-stripped body
