@@ -1,17 +1,19 @@
 #!/bin/bash
 # HBM traffic of the config-4 stream kernels: separate rocprofv3 --pmc passes
 # (FETCH_SIZE, WRITE_SIZE) over tools/stream_bench.py, summarised per kernel
-# (mean over its dispatches) into gpurun_out/pmc_stream.json.
+# (mean over its dispatches) into gpurun_out/pmc_stream${SUF}.json; extra
+# arguments go to stream_bench.py (e.g. SUF=_i16 tools/pmc_stream.sh --i16).
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $R/gpurun_out
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmcs_fetch -o run -- python3 tools/stream_bench.py --reps 1 > $R/gpurun_out/pmcs_fetch.log 2>&1 && \
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmcs_write -o run -- python3 tools/stream_bench.py --reps 1 > $R/gpurun_out/pmcs_write.log 2>&1 && \
-python3 - <<'PY' > $R/gpurun_out/pmc_stream.json
-import csv, glob, json, collections
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmcs_fetch$SUF -o run -- python3 tools/stream_bench.py --reps 1 "$@" > $R/gpurun_out/pmcs_fetch$SUF.log 2>&1 && \
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmcs_write$SUF -o run -- python3 tools/stream_bench.py --reps 1 "$@" > $R/gpurun_out/pmcs_write$SUF.log 2>&1 && \
+SUF=$SUF python3 - <<'PY' > $R/gpurun_out/pmc_stream$SUF.json
+import csv, glob, json, collections, os
+suf = os.environ.get("SUF", "")
 acc = collections.defaultdict(list)
-for ctr, path in (("FETCH_SIZE", "gpurun_out/pmcs_fetch/run_counter_collection.csv"),
-                  ("WRITE_SIZE", "gpurun_out/pmcs_write/run_counter_collection.csv")):
+for ctr, path in (("FETCH_SIZE", f"gpurun_out/pmcs_fetch{suf}/run_counter_collection.csv"),
+                  ("WRITE_SIZE", f"gpurun_out/pmcs_write{suf}/run_counter_collection.csv")):
     for r in csv.DictReader(open(path)):
         k = r["Kernel_Name"]
         for key in ("stream_walk_kernel", "compact_kernel", "cfo_kernel", "stream_params_kernel", "stream_sync_kernel",
