@@ -1477,7 +1477,12 @@ __global__ void __launch_bounds__(128, 4) stream_decode_kernel(CfoArgs c, Stream
     for (int i = 0; i < RX_DPT; ++i) pk[i] = r.tab.rx_pack[lane0 + 64 * i];
     const int pbin = r.tab.pilot_swz[lane0];
     double2* chan = a.chan_out + f * D;
+    // the sync stage's dependent chains issue ahead of the transform-heavy
+    // rx stage of the CU's other frames (priority 1 vs 0: 498 -> 478 us;
+    // 2 and 3 gain less)
+    __builtin_amdgcn_s_setprio(1);
     sync_frame(c, a, f, Ls, chan, corr, true);
+    __builtin_amdgcn_s_setprio(0);
     rx2_frame<I16>(r, f, Lr, corr, pk, pbin, chan);
 }
 
@@ -2072,6 +2077,21 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
             if (past || pos >= end + a.ext) break;
         }
         const long spos = pos;  // this step's start state
+        {
+            // issue priority by the work left: walkers further from their
+            // core end go first. The arbiter otherwise favours the oldest
+            // resident wave, whatever its progress: equal chunks finished in
+            // dispatch order (253 us for a CU's first walker, 325 us for its
+            // eighth), and the CUs drained slowly (walker 386 -> 365 us)
+            const long left = end - pos, span = end - core0 + a.halo;
+            const int pr = left <= 0 ? 0 : (int)min(3L, left * 4 / max(1L, span));
+            switch (__builtin_amdgcn_readfirstlane(pr)) {
+                case 3: __builtin_amdgcn_s_setprio(3); break;
+                case 2: __builtin_amdgcn_s_setprio(2); break;
+                case 1: __builtin_amdgcn_s_setprio(1); break;
+                default: __builtin_amdgcn_s_setprio(0); break;
+            }
+        }
         // find_t2sin(pos): blocks pos + k*N, first hit wins
         long hit = -1;
         bool stop = false;
