@@ -523,7 +523,7 @@ def main():
             "mod_type": p["mod_type"], "frames_per_gpu": nf, "symbols_per_gpu": nf * S,
             "total_frames": args.total_frames if strong else world * nf,
             "samples_per_step_per_gpu": nf * msg, "parallelism": f"frame-sharded x{world}",
-            "backend": args.backend if world > 1 else None,
+            "backend": args.backend if dist else None,
         },
         "roofline": {
             "bound": "hbm",

@@ -29,7 +29,7 @@ def env_world() -> tuple[int, int, int]:
 def reduce_counters(counters, dist=None):
     """SUM all-reduce of an int64 tensor [bit_errors, bits, samples, frames]
     (in place; a GPU tensor under gloo is reduced through a host copy)."""
-    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist is not None and dist.is_initialized():
         if dist.get_backend() == "gloo" and counters.is_cuda:
             h = counters.cpu()
             dist.all_reduce(h)
@@ -42,7 +42,7 @@ def reduce_counters(counters, dist=None):
 def max_over_ranks(value: float, device, dist=None) -> float:
     import torch
     t = torch.tensor([value], dtype=torch.float64, device=collective_device(dist, device))
-    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist is not None and dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -97,7 +97,9 @@ def init(backend: str, local_rank: int, use_gpu: bool = True):
                                "use --backend gloo to rehearse several ranks on one GPU")
         dev = torch.device("cuda", local_rank % max(ndev, 1))
         torch.cuda.set_device(dev)
-    if world == 1:
+    # a launched job (WORLD_SIZE set) joins the group even at one rank, so the
+    # RCCL reduction path runs under `torch.distributed.run --nproc-per-node 1`
+    if world == 1 and "WORLD_SIZE" not in os.environ:
         return None, dev
     import torch.distributed as dist
     if backend == "nccl":

@@ -44,7 +44,7 @@ def main():
     else:
         seen = [(rank, world, b, c, out.tobytes().hex())]
     if rank == 0:
-        print(json.dumps({"n_gpus": world, "totals": counters.tolist(), "max_elapsed": elapsed,
+        print(json.dumps({"n_gpus": world, "grouped": dist is not None, "totals": counters.tolist(), "max_elapsed": elapsed,
                           "ranks": [[r, w, b, c] for r, w, b, c, _ in seen],
                           "bytes_hex": "".join(h for *_, h in sorted(seen))}), flush=True)
     if dist:

@@ -109,6 +109,24 @@ def test_launcher_starts_ranks_and_reduction_equals_single_rank():
     assert bytes.fromhex(res["bytes_hex"]) == out1.tobytes()
 
 
+def test_launched_single_rank_joins_the_group():
+    """Under torch.distributed.run at one rank (WORLD_SIZE=1 in the
+    environment) the rank still joins the process group, so the reduction
+    path (RCCL on the GPU box) runs; the totals equal the unlaunched run's."""
+    import json
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dist_job_cpu.py")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    rc, out = ofdm_dist.launch_ranks(1, script, ["--frames", str(NF)], env=env, capture=True)
+    assert rc == 0, out
+    res = json.loads([ln for ln in out.splitlines() if ln.startswith("{")][0])
+    assert res["n_gpus"] == 1 and res["grouped"] and res["max_elapsed"] == 1.0
+    g = O.geometry(D)
+    data = np.random.default_rng(5).integers(0, 256, NF * g["bytes_per_frame"], dtype=np.uint8)
+    iq = O.awgn(O.tx_batch(D, data, NF), 0.45, seed=7)
+    _, out1, errs = O.rx_batch(D, iq, NF, g["message_len"], ref=data)
+    assert res["totals"] == [errs, NF * g["bytes_per_frame"] * 8, NF * g["message_len"], NF]
+
+
 def test_bench_gpus_flag_launches_ranks(monkeypatch):
     """bench.py --gpus 4 without a launcher environment hands off to
     ofdm_dist.launch_ranks with its own path and argv (before any GPU call)."""
