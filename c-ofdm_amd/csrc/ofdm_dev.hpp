@@ -4,10 +4,27 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <mutex>
+#include <set>
+#include <utility>
 
 #include "ofdm_fft.hpp"
 
 namespace ofdm {
+
+// Host side: opt a kernel into `bytes` of dynamic LDS once per (kernel,
+// device). The launch helpers run on any host thread (one context per thread,
+// or two contexts on two streams) and on any device of the process.
+inline void lds_opt_in(const void* fn, int bytes)
+{
+    static std::mutex mu;
+    static std::set<std::pair<const void*, int>> done;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    std::lock_guard<std::mutex> g(mu);
+    if (done.insert({fn, dev}).second)
+        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
 
 // Modulation::demod decision for one point (modulation.cpp:62-84): BPSK
 // re+im > 0; QAM clamp to [-1,1] then uint8((v+1)*str_size_1 + 0.5) per axis,

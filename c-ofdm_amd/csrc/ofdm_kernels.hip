@@ -1010,12 +1010,7 @@ static hipError_t tx_launch_n(const TxArgs& a, hipStream_t st)
 {
     using FS = FftShape<LOGN>;
     const size_t shm = sizeof(double2) * (FS::PADN + TwLds<LOGN>::SIZE + TX_LDS_ZERO + 1) + FS::N;  // + points + payload
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)tx_kernel<LOGN, POINTS, NOISE, I16>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-        attr = true;
-    }
+    lds_opt_in((const void*)tx_kernel<LOGN, POINTS, NOISE, I16>, (int)shm);
     const long nsym = a.nframes * a.S;
     if (nsym <= 0) return hipSuccess;
     // persistent grid: enough workgroups to fill every CU several times over
@@ -1088,12 +1083,7 @@ static hipError_t rx_launch_n(const RxArgs& a, hipStream_t st)
     using FS = FftShape<LOGN>;
     const size_t shm = rx_shm<LOGN>(a);
     if (shm > 160 * 1024) return hipErrorInvalidValue;
-    static int attr = 0;
-    if ((size_t)attr < shm) {
-        (void)hipFuncSetAttribute((const void*)rx_kernel<LOGN, STAGED, I16, SYNC>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr = 160 * 1024;
-    }
+    lds_opt_in((const void*)rx_kernel<LOGN, STAGED, I16, SYNC>, 160 * 1024);
     if (a.nframes <= 0) return hipSuccess;
     // persistent: RX_WAVES_PER_CU resident waves per CU (the register
     // window's occupancy: 2 per SIMD), as far as LDS allows
@@ -1113,12 +1103,7 @@ static hipError_t rx_stream2_launch(const RxArgs& a, hipStream_t st)
 {
     const size_t shm = sizeof(double2) * (2 * 512 + TwLds<9>::SIZE + 2 * (size_t)a.S * a.P + a.D) + 2 * sizeof(double);
     if (shm > 160 * 1024) return hipErrorInvalidValue;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)rx_stream2_kernel<I16>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        attr = true;
-    }
+    lds_opt_in((const void*)rx_stream2_kernel<I16>, 160 * 1024);
     if (a.nframes <= 0) return hipSuccess;
     // persistent: 12 waves per CU (3 per SIMD: 155 VGPRs) = 6 workgroups, as far as LDS allows
     long per_cu = (long)(160 * 1024) / (long)shm;

@@ -252,12 +252,7 @@ static hipError_t t2_launch_n(const T2Args& a, hipStream_t st)
 {
     using Geo = T2Geo<LOGN>;
     const size_t shm = sizeof(double2) * (TwLds<LOGN>::SIZE + 2 * Geo::G * (Geo::T / 64 + 1) + Geo::G * Geo::N);
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)t2_scan_kernel<LOGN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        attr = true;
-    }
+    lds_opt_in((const void*)t2_scan_kernel<LOGN>, 160 * 1024);
     const long grid = (a.nblocks + Geo::G - 1) / Geo::G;
     hipLaunchKernelGGL(t2_scan_kernel<LOGN>, dim3((unsigned)grid), dim3(Geo::NT), shm, st, a);
     return hipGetLastError();
@@ -361,12 +356,7 @@ hipError_t launch_find_preamble(const PreambleArgs& a, hipStream_t st)
     if (a.nstarts <= 0) return hipSuccess;
     const size_t shm = sizeof(double2) * (a.cycles + 2 * (size_t)a.L) + sizeof(double) * a.cycles + 16;
     if (shm > 160 * 1024) return hipErrorInvalidValue;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)find_preamble_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        attr = true;
-    }
+    lds_opt_in((const void*)find_preamble_kernel, 160 * 1024);
     hipLaunchKernelGGL(find_preamble_kernel, dim3((unsigned)a.nstarts), dim3(SYNC_THREADS), shm, st, a);
     return hipGetLastError();
 }
@@ -502,12 +492,7 @@ static hipError_t cfo_launch_n(const CfoArgs& a, hipStream_t st)
     const size_t shm = sizeof(double2) * (TwLds<LOGM>::SIZE + (size_t)G * M) + sizeof(double) * G * M +
                        sizeof(int) * (a.P + 2) + 16;
     if (shm > 160 * 1024) return hipErrorInvalidValue;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)cfo_kernel<LOGM, G>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        attr = true;
-    }
+    lds_opt_in((const void*)cfo_kernel<LOGM, G>, 160 * 1024);
     hipLaunchKernelGGL((cfo_kernel<LOGM, G>), dim3((unsigned)a.nframes), dim3(NT), shm, st, a);
     return hipGetLastError();
 }
@@ -716,12 +701,7 @@ static hipError_t chan_launch_n(const ChanArgs& a, hipStream_t st)
     const size_t shm = sizeof(double2) * (TwLds<LOGN>::SIZE + FS::N + (size_t)a.npr * a.P + a.D / 2 + 1) +
                        sizeof(double) * (a.D / 2 + 2) + sizeof(double2) * 40;
     if (shm > 160 * 1024) return hipErrorInvalidValue;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)chan_kernel<LOGN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        attr = true;
-    }
+    lds_opt_in((const void*)chan_kernel<LOGN>, 160 * 1024);
     hipLaunchKernelGGL(chan_kernel<LOGN>, dim3((unsigned)a.nframes), dim3(FS::T), shm, st, a);
     return hipGetLastError();
 }
@@ -1009,12 +989,7 @@ static hipError_t params_launch_n(const StreamParamsArgs& a, hipStream_t st)
     const size_t shm = sizeof(double2) * (TwLds<LOGN>::SIZE + FS::N + (size_t)a.P + ndat) +
                        sizeof(double) * (a.D / 2 + 2) + sizeof(double2) * 32 + sizeof(double) * 130;
     if (shm > 160 * 1024) return hipErrorInvalidValue;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)stream_params_kernel<LOGN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        attr = true;
-    }
+    lds_opt_in((const void*)stream_params_kernel<LOGN>, 160 * 1024);
     hipLaunchKernelGGL(stream_params_kernel<LOGN>, dim3((unsigned)a.nframes), dim3(FS::T), shm, st, a);
     return hipGetLastError();
 }
@@ -1499,12 +1474,7 @@ static hipError_t decode_launch(const CfoArgs& c, const StreamParamsArgs& a, con
     const size_t shm = sizeof(double2) * (TwLds<9>::SIZE + 1024) + sizeof(double) * 4 * a.S +
                        std::max(sizeof(double2) * (2 * (size_t)a.S * a.P) + sizeof(double) * 2,
                                 sizeof(double2) * (a.P + 32 + 1 + a.S) + sizeof(double) * 132 + sizeof(int) * (a.P + 2));
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)stream_decode_kernel<I16>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        attr = true;
-    }
+    lds_opt_in((const void*)stream_decode_kernel<I16>, 160 * 1024);
     hipLaunchKernelGGL(stream_decode_kernel<I16>, dim3((unsigned)a.nframes), dim3(128), shm, st, c, a, r);
     return hipGetLastError();
 }
@@ -1524,12 +1494,7 @@ hipError_t launch_stream_sync(const CfoArgs& c, const StreamParamsArgs& a, int l
     if (!stream_sync_geometry(c, a, logn, logm, g)) return hipErrorNotSupported;  // the two-kernel path covers other geometries
     const size_t shm = sizeof(double2) * (TwLds<9>::SIZE + TwLds<7>::SIZE + 640 + a.P + (a.D / 2 + 1) + 32 + 1 + a.S) +
                        sizeof(double) * (a.D / 2 + 2 + 64 + 64 + 4) + sizeof(int) * (a.P + 2);
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)stream_sync_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        attr = true;
-    }
+    lds_opt_in((const void*)stream_sync_kernel, 160 * 1024);
     hipLaunchKernelGGL(stream_sync_kernel, dim3((unsigned)a.nframes), dim3(128), shm, st, c, a);
     return hipGetLastError();
 }
@@ -2337,12 +2302,7 @@ static hipError_t walk_launch_n(const WalkArgs& a, long nblocks, hipStream_t st)
 {
     const size_t shm = walk_shm<LOGT>(a.L, a.cycles, a.tspec != nullptr);
     if (shm > 160 * 1024) return hipErrorInvalidValue;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)stream_walk_kernel<LOGT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        attr = true;
-    }
+    lds_opt_in((const void*)stream_walk_kernel<LOGT>, 160 * 1024);
     hipLaunchKernelGGL(stream_walk_kernel<LOGT>, dim3((unsigned)nblocks), dim3(WalkShape<LOGT>::WT), shm, st, a);
     return hipGetLastError();
 }
@@ -2352,12 +2312,13 @@ static long walk_slots_n(int L, int C, bool fft)
 {
     int dev = 0, ncu = 0, per = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    static std::mutex mu;           // contexts on several host threads query it
     static long cache[64][4] = {};  // device: {L, C, fft, slots} of the last query
+    std::lock_guard<std::mutex> g(mu);
     long* q = cache[dev];
     if (q[3] && q[0] == L && q[1] == C && q[2] == (long)fft) return q[3];
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
-    (void)hipFuncSetAttribute((const void*)stream_walk_kernel<LOGT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+    lds_opt_in((const void*)stream_walk_kernel<LOGT>, 160 * 1024);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)stream_walk_kernel<LOGT>, WalkShape<LOGT>::WT,
                                                      walk_shm<LOGT>(L, C, fft)) != hipSuccess ||
         per <= 0)
