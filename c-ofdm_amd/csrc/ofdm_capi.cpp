@@ -1395,20 +1395,14 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     long* rec = reinterpret_cast<long*>(hb);
     long* ex = reinterpret_cast<long*>(hb + rec_b);
     int* nrec = reinterpret_cast<int*>(ex + nchunks + 2);
-    // the copy runs on a side stream, so the compaction and the decode on the
-    // caller's stream do not queue behind it
     if (!c->ev_walk) HIP_TRY(hipEventCreateWithFlags(&c->ev_walk, hipEventDisableTiming));
     if (!c->ev_wdone) HIP_TRY(hipEventCreateWithFlags(&c->ev_wdone, hipEventDisableTiming));
+    if (!c->ev_qreset) HIP_TRY(hipEventCreateWithFlags(&c->ev_qreset, hipEventDisableTiming));
     if (!c->side) HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
-    HIP_TRY(hipEventRecord(c->ev_wdone, st));
-    HIP_TRY(hipStreamWaitEvent(c->side, c->ev_wdone, 0));
-    HIP_TRY(hipMemcpyAsync(hb, wb, walk_b, hipMemcpyDeviceToHost, c->side));
-    HIP_TRY(hipEventRecord(c->ev_walk, c->side));
     // Speculative decode: every chunk's in-core records, compacted on the
-    // device behind the copy of the walk records, are decoded while the host
-    // stitches the walks. That list is the stitched walk unless a chunk needs
-    // a re-walk (or the walk ends early); then the host's list is decoded
-    // again over it.
+    // device behind the walk, are decoded while the host stitches the walks.
+    // That list is the stitched walk unless a chunk needs a re-walk (or the
+    // walk ends early); then the host's list is decoded again over it.
     const size_t ub = std::min(max_frames, (size_t)nchunks * max_rec);
     const bool spec = fused && ub > 0 && ub * per <= ((size_t)256 << 20);
     long* d_pbs = nullptr;
@@ -1428,11 +1422,22 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
         ka.queue_reset = c->d_queue;  // after the walk (stream order): zero for the next call
         e = ofdm::launch_compact(ka, st);
         if (e != hipSuccess) return hip_fail(e, "stream compact launch");
-        if (!c->ev_qreset) HIP_TRY(hipEventCreateWithFlags(&c->ev_qreset, hipEventDisableTiming));
+    }
+    // The walk records go to the host on a side stream, so the decode on the
+    // caller's stream does not queue behind the copy. The one event marks the
+    // walk and the compaction together: a marker between two dependent
+    // kernels costs a launch gap, so walk -> compaction runs back to back.
+    HIP_TRY(hipEventRecord(c->ev_wdone, st));
+    HIP_TRY(hipStreamWaitEvent(c->side, c->ev_wdone, 0));
+    HIP_TRY(hipMemcpyAsync(hb, wb, walk_b, hipMemcpyDeviceToHost, c->side));
+    HIP_TRY(hipEventRecord(c->ev_walk, c->side));
+    if (spec) {
+        if ((rc = decode_fused(d_pbs, ub, d_pbs + ub))) return rc;
+        // the queue counter was zeroed by the compaction: the decode is behind
+        // it in stream order, so the event can follow the decode's launch
         HIP_TRY(hipEventRecord(c->ev_qreset, st));
         c->queue_zero = true;
     }
-    if (spec && (rc = decode_fused(d_pbs, ub, d_pbs + ub))) return rc;
     HIP_TRY(hipEventSynchronize(c->ev_walk));
 
     // the speculative list, from the walks as they came back
