@@ -148,27 +148,36 @@ def load_pmc_stream(workload: str):
     return best
 
 
-def cpu_stream_baseline(p, x_host: np.ndarray, budget_s: float):
+def cpu_stream_baseline(p, x_host: np.ndarray, budget_s: float, i16: bool = False):
     """The oracle's rx.cpp walk + main.cpp:60-80 decode, single-threaded as the
-    reference's rx runs, over a prefix of the same stream sized to ~budget_s."""
+    reference's rx runs, over a prefix of the same stream sized to ~budget_s.
+    i16: x_host is the interleaved complex<int16> wire stream, converted to
+    complex<double> inside the timed region (FRAME_FORM::form_int16_to_double,
+    rx.cpp:81-90), as the reference's receiver does before its walk."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     g = O.geometry(p)
     span = g["preamble_len"] + g["message_len"]
     n = 1 << 18
+    total = len(x_host) // 2 if i16 else len(x_host)
     while True:
-        h = x_host[:n]
         t0 = time.perf_counter()
+        if i16:
+            w = x_host[:2 * n].astype(np.float64)
+            h = w[0::2] + 1j * w[1::2]
+        else:
+            h = x_host[:n]
         pbs = O.stream_walk(p, h)
         for pb in pbs:
             if pb + span <= len(h):
                 O.decode_frame(p, h[pb:pb + span])
         dt = time.perf_counter() - t0
-        if dt > budget_s / 3 or n >= len(x_host):
+        if dt > budget_s / 3 or n >= total:
             break
-        n = min(len(x_host), n * 4)
+        n = min(total, n * 4)
+    conv = "int16 -> f64 conversion + " if i16 else ""
     return {"value": n / dt, "unit": "stream samples/s", "cores": 1, "kind": "port",
-            "sample": f"oracle orc_stream_walk + orc_decode_frame (own FFT; FFTW absent) over the first {n} "
+            "sample": f"{conv}oracle orc_stream_walk + orc_decode_frame (own FFT; FFTW absent) over the first {n} "
                       f"samples ({len(pbs)} frames) of the same stream in {dt:.1f} s, 1 thread "
                       f"(rx.cpp's loop is single-threaded) on {_cpu_model()}"}
 
@@ -258,9 +267,10 @@ def stream_leg(args, dist, dev, world, rank, M, i16: bool):
     if world == 1 and args.stream_pipeline > 1:
         res["pipelined"] = stream_pipelined(args, p, M, dev, modem, layout, rx, walk, outs, x, nsl, cap, i16,
                                             n_owned, exchange, SS)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not i16:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            res["cpu_baseline"] = cpu_stream_baseline(p, x[:1 << 27].cpu().numpy(), args.stream_cpu_budget)
+            res["cpu_baseline"] = cpu_stream_baseline(p, x[:(2 << 27) if i16 else (1 << 27)].cpu().numpy(),
+                                                      args.stream_cpu_budget, i16=i16)
         except Exception as e:  # reported, not fatal
             res["cpu_baseline"] = {"error": repr(e)}
     modem.close()
@@ -415,6 +425,10 @@ def main():
                     help="contexts for the stream record's pipelined figure (1: off; one GPU only)")
     ap.add_argument("--no-config3", action="store_true", help="skip the config-3 (config C) sub-record")
     ap.add_argument("--config3-frames", type=int, default=4096, help="config C frames per GPU (weak)")
+    ap.add_argument("--check-frames", default="",
+                    help="comma-separated GLOBAL frame indices: after the timed steps each rank holding one writes "
+                         "its noisy IQ, decoded bytes and constellation to --check-out (parity tests)")
+    ap.add_argument("--check-out", default="", help="directory for the --check-frames dumps (rank<r>.npz)")
     args = ap.parse_args()
 
     import ofdm_dist
@@ -545,6 +559,21 @@ def main():
         "frames": int(tot[3]),
         "cpu_baseline": None,
     }
+    if args.check_frames:
+        # outside the timed region: the last step's noisy IQ (tx is a pure
+        # function of the global frame / sample index) and its rx outputs
+        torch.cuda.synchronize(dev)
+        want = sorted({int(v) for v in args.check_frames.split(",") if v.strip()})
+        mine = [g for g in want if f0 <= g < f0 + nf]
+        dump = {"frames": np.array(mine, dtype=np.int64)}
+        for g in mine:
+            lf = g - f0
+            dump[f"iq_{g}"] = iq[lf * msg:(lf + 1) * msg].cpu().numpy()
+            dump[f"bytes_{g}"] = out[lf * bpf:(lf + 1) * bpf].cpu().numpy()
+            dump[f"constell_{g}"] = cons[lf * npts:(lf + 1) * npts].cpu().numpy()
+        os.makedirs(args.check_out, exist_ok=True)
+        np.savez(os.path.join(args.check_out, f"rank{rank}.npz"), **dump)
+        result["check"] = {"frames": want, "noise_std": noise_std, "seed": 1, "message_len": msg}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             cpus = granted_cpus()

@@ -158,7 +158,15 @@ struct ofdm_ctx {
     hipStream_t h_frames_stream = nullptr;  // stream of the last copy out of h_frames
     bool h_frames_used = false;
     int* d_queue = nullptr;        // walker chunk counter (zero between calls)
-    int* d_rxq = nullptr;          // rx dynamic-frame counters {next, done}, zero between launches
+    // rx dynamic-frame counters {next, done}, zero between launches: one slot
+    // per HIP stream that launched rx on this context (launches on one stream
+    // run in order, so each slot is reset by the launch before the next uses
+    // it); streams past RX_QUEUE_SLOTS run with a static frame order
+    static constexpr int RX_QUEUE_SLOTS = 32;
+    int* d_rxq = nullptr;          // RX_QUEUE_SLOTS x 16 ints (one 64-B line each)
+    hipStream_t rxq_stream[RX_QUEUE_SLOTS] = {};
+    int rxq_used = 0;
+    ofdm_walk_tuning walk{};       // stream walker settings (ofdm_set_walk_tuning)
     bool queue_zero = false;       // the last call's compaction resets it ...
     hipEvent_t ev_qreset = nullptr;  // ... when this event completes
     hipEvent_t ev_walk = nullptr;  // walk records landed in h_walk
@@ -574,15 +582,35 @@ int ofdm_create(const ofdm_params* params, int device, ofdm_ctx** out)
         }
     }
     // rx dynamic-frame counters: zero now, and left zero by every rx launch
-    hipError_t qe = hipMalloc((void**)&c->d_rxq, 2 * sizeof(int));
-    if (qe == hipSuccess) qe = hipMemset(c->d_rxq, 0, 2 * sizeof(int));
+    const size_t qbytes = ofdm_ctx::RX_QUEUE_SLOTS * 16 * sizeof(int);
+    hipError_t qe = hipMalloc((void**)&c->d_rxq, qbytes);
+    if (qe == hipSuccess) qe = hipMemset(c->d_rxq, 0, qbytes);
     if (qe == hipSuccess) qe = hipDeviceSynchronize();
     if (qe != hipSuccess) {
         ofdm_destroy(c);
         return hip_fail(qe, "rx frame counters");
     }
+    ofdm_walk_tuning_default(&c->walk);
     *out = c;
     return OFDM_OK;
+}
+
+// The rx frame-queue slot of `st` (nullptr: no slot free, static frame order).
+static int* rx_queue(ofdm_ctx* c, hipStream_t st)
+{
+    for (int i = 0; i < c->rxq_used; ++i)
+        if (c->rxq_stream[i] == st) return c->d_rxq + 16 * i;
+    if (c->rxq_used == ofdm_ctx::RX_QUEUE_SLOTS) return nullptr;
+    c->rxq_stream[c->rxq_used] = st;
+    return c->d_rxq + 16 * c->rxq_used++;
+}
+
+// A launch that did not start leaves its slot as it was (zero). One that
+// faulted poisons the context anyway (HIP errors are sticky); the slot is
+// still zeroed so a recovered context starts clean.
+static void rx_queue_reset(ofdm_ctx* c, int* q, hipStream_t st)
+{
+    if (q) (void)hipMemsetAsync(q, 0, 2 * sizeof(int), st);
 }
 
 // pilot_freq_sinh plan for a form of nsym symbols: S = (N+cp)*nsym = M or 5*M,
@@ -810,9 +838,7 @@ static int rx_demod_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, siz
     a.k = c->k;
     a.bytes_per_frame = c->geo.bytes_per_frame;
     a.pilot_ampl = (double)c->p.pilot_ampl / 1000;
-#ifndef OFDM_RX_NOQUEUE  // timing experiment only: static frame order
-    a.queue = c->d_rxq;
-#endif
+    a.queue = rx_queue(c, (hipStream_t)stream);
     const bool fits = c->S <= ofdm::RX_SMAX && c->D <= ofdm::RX_DPT * (c->N / 8);
     if (!fits) {
         if (c->D > ofdm::RX_DPT * (c->N / 8))
@@ -833,7 +859,10 @@ static int rx_demod_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, siz
         }
     }
     hipError_t e = ofdm::launch_rx(c->logn, a, (hipStream_t)stream, nullptr);
-    if (e != hipSuccess) return hip_fail(e, "rx_kernel launch");
+    if (e != hipSuccess) {
+        rx_queue_reset(c, a.queue, (hipStream_t)stream);
+        return hip_fail(e, "rx_kernel launch");
+    }
     return OFDM_OK;
 }
 
@@ -907,10 +936,13 @@ int ofdm_fft_read(ofdm_ctx* c, const double* fft_buf, size_t nframes, double* re
     a.k = c->k;
     a.bytes_per_frame = c->geo.bytes_per_frame;
     a.pilot_ampl = (double)c->p.pilot_ampl / 1000;
-    a.queue = c->d_rxq;
+    a.queue = rx_queue(c, (hipStream_t)stream);
     if (!(c->S <= ofdm::RX_SMAX && c->D <= ofdm::RX_DPT * (c->N / 8))) a.ystage = a.constell;
     hipError_t e = ofdm::launch_rx(c->logn, a, (hipStream_t)stream, nullptr);
-    if (e != hipSuccess) return hip_fail(e, "fft_read launch");
+    if (e != hipSuccess) {
+        rx_queue_reset(c, a.queue, (hipStream_t)stream);
+        return hip_fail(e, "fft_read launch");
+    }
     return OFDM_OK;
 }
 
@@ -1172,28 +1204,26 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     // chunks cost less), each >= 8 frames
     const long slots = ofdm::stream_walk_slots(c->t2_logn, (int)c->p.pr_sin_len,
                                                (int)(2 * c->p.t2sin_size + c->p.pr_sin_len), c->d_tspec != nullptr);
-    // Knobs (environment, for experiments and tests): chunks per walker slot,
+    // Per-context tuning (ofdm_set_walk_tuning): chunks per walker slot,
     // walk-in halo and walk-on extension in 1/1000 frames. Defaults: one
     // chunk per slot, 3-frame halo, no extension (tools/walk_q_sweep.sh:
     // 1.5-frame halos with a 2-frame extension, or 2-3 chunks per slot, gain
     // nothing measurable on config 4; shorter halos force re-walks).
-    const char* eq = getenv("OFDM_WALK_Q");
-    const char* eh = getenv("OFDM_WALK_HALO");
-    const long qper = eq ? std::max(1L, atol(eq)) : 1;
+    const ofdm_walk_tuning& tu = c->walk;
+    const long qper = std::max(1L, tu.chunks_per_slot);
     const long span_w = own_hi - own_lo;  // the chunk cores tile [own_lo, own_hi)
     if (chunk <= 0) chunk = std::max(8 * flen, (span_w + slots * qper - 1) / (slots * qper));
     chunk = std::max(chunk, (long)c->t2);
-    const long halo = eh ? std::max(0L, atol(eh)) * flen / 1000 : 3 * flen;
-    const char* ee = getenv("OFDM_WALK_EXT");
-    const long ext = ee ? std::max(0L, atol(ee)) * flen / 1000 : 0;
+    const long halo = std::max(0L, tu.halo_milli) * flen / 1000;
+    const long ext = std::max(0L, tu.ext_milli) * flen / 1000;
     const long nchunks = std::max(1L, (span_w + chunk - 1) / chunk);
     if (nchunks > 1 << 20) return fail(OFDM_ERR_INVALID, "chunk too small for this stream");
     // each located frame advances the walk by > message_len, and a walker can
-    // walk on past its core end by ext plus one scan step (256 threads x 8
+    // walk on past its core end by ext plus one scan step (WALK_SCAN_MAX
     // samples) and the preamble window: this many records always suffice
     // (chunk 0 walks in from `start`, the others a halo before their core)
     const int max_rec =
-        (int)((chunk + std::max(halo, own_lo - start) + std::max(ext, 2 * flen) + 2048 + 2 * c->p.t2sin_size +
+        (int)((chunk + std::max(halo, own_lo - start) + std::max(ext, 2 * flen) + ofdm::WALK_SCAN_MAX + 2 * c->p.t2sin_size +
                c->p.pr_sin_len) / msg + 4);
     int rc;
     const size_t rec_b = (size_t)nchunks * max_rec * sizeof(long);
@@ -1210,10 +1240,7 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     int* d_first_in = d_ncore + nchunks;
 
     ofdm::WalkArgs w{};
-    {
-        const char* ex = getenv("OFDM_WALK_EXACT");  // test hook: certified fast search off
-        w.exact_only = ex && ex[0] == '1';
-    }
+    w.exact_only = tu.exact_search != 0;
     w.tw_m = c->d_twm;
     w.tspec = c->d_tspec;  // nullptr: direct certified search
     w.tspec_max = c->tspec_max;
@@ -1227,16 +1254,9 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     w.a2 = std::max(0, f2 - sm);
     w.b2 = std::min(c->t2 - 1, f2 + sm);
     w.t2_level = (double)c->p.t2_sin_level / 1000;
-    // FP32 T2 screen (certified, FP64 re-evaluation of uncertain steps).
-    // Test / experiment hooks: OFDM_WALK_T2_F32=0 turns it off,
-    // OFDM_WALK_T2_MARGIN overrides the certification margin (1 makes every
-    // block uncertain, i.e. every step is decided by the FP64 path).
-    {
-        const char* e32 = getenv("OFDM_WALK_T2_F32");
-        const char* em = getenv("OFDM_WALK_T2_MARGIN");
-        w.t2_f32 = !(e32 && e32[0] == '0');
-        w.t2_margin = em ? atof(em) : 4e-5;
-    }
+    // FP32 T2 screen (certified, FP64 re-evaluation of uncertain steps)
+    w.t2_f32 = tu.t2_f32 != 0;
+    w.t2_margin = tu.t2_margin;
     w.templ = c->d_templ;
     w.L = (int)c->p.pr_sin_len;
     w.cycles = (int)(2 * c->p.t2sin_size + c->p.pr_sin_len);
@@ -1361,25 +1381,14 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
             // 512, 640-point CFO form: sync stage + rx stage per frame, the
             // ramps and channel through LDS); else pilot_freq_sinh + the
             // params stage (one kernel or two), then the stream rx.
-            hipError_t e2 = hipErrorNotSupported;
-#ifndef OFDM_STREAM_SYNC2  // timing experiment only: the staged launches
-            e2 = ofdm::launch_stream_decode(ca, sa, ra, c->logn, pl->logm, pl->g, st);
-#endif
+            hipError_t e2 = ofdm::launch_stream_decode(ca, sa, ra, c->logn, pl->logm, pl->g, st);
             if (e2 == hipErrorNotSupported) {
-                // one kernel for pilot_freq_sinh + the params stage where the
-                // geometry allows (N = 512, 640-point CFO form), else two
-                e2 = hipErrorNotSupported;
-#ifndef OFDM_STREAM_SYNC2  // timing experiment only: the two-kernel path
-                e2 = ofdm::launch_stream_sync(ca, sa, c->logn, pl->logm, pl->g, st);
-#endif
-                if (e2 == hipErrorNotSupported) {
-                    e2 = ofdm::launch_cfo(pl->logm, pl->g, ca, st);
-                    if (e2 != hipSuccess) return hip_fail(e2, "stream cfo launch");
-                    e2 = ofdm::launch_stream_params(c->logn, sa, st);
-                    if (e2 != hipSuccess) return hip_fail(e2, "stream params launch");
-                } else if (e2 != hipSuccess) {
-                    return hip_fail(e2, "stream sync launch");
-                }
+                // other geometries: pilot_freq_sinh, the params stage, then
+                // the stream rx (two waves per frame at N = 512)
+                e2 = ofdm::launch_cfo(pl->logm, pl->g, ca, st);
+                if (e2 != hipSuccess) return hip_fail(e2, "stream cfo launch");
+                e2 = ofdm::launch_stream_params(c->logn, sa, st);
+                if (e2 != hipSuccess) return hip_fail(e2, "stream params launch");
                 e2 = ofdm::launch_rx(c->logn, ra, st, nullptr);
                 if (e2 != hipSuccess) return hip_fail(e2, "stream rx launch");
             } else if (e2 != hipSuccess) {
@@ -1589,6 +1598,45 @@ int ofdm_rx_stream_i16(ofdm_ctx* c, const int16_t* iq16, size_t n, size_t max_fr
     if (!iq16) return fail(OFDM_ERR_INVALID, "null argument");
     return rx_stream_impl(c, nullptr, iq16, n, max_frames, chunk, pb_out, bytes_out, constell_out, cfo_out,
                           nframes_out, stream, 0, 0, (long)n, nullptr, 0, nullptr, nullptr);
+}
+
+int ofdm_stream_shard_margins(const ofdm_ctx* c, long* halo_out, long* tail_out)
+{
+    if (!c) return fail(OFDM_ERR_INVALID, "null ctx");
+    const long flen = c->geo.frame_len, window = 2 * c->p.t2sin_size + c->p.pr_sin_len;
+    if (halo_out) *halo_out = std::max(std::max(0L, c->walk.halo_milli) * flen / 1000, flen + window + c->t2);
+    if (tail_out)
+        *tail_out = ofdm::WALK_SCAN_MAX + c->t2 + window + c->geo.preamble_len + c->geo.message_len + 1;
+    return OFDM_OK;
+}
+
+int ofdm_walk_tuning_default(ofdm_walk_tuning* o)
+{
+    if (!o) return fail(OFDM_ERR_INVALID, "null argument");
+    *o = ofdm_walk_tuning{};
+    o->chunks_per_slot = 1;
+    o->halo_milli = 3000;
+    o->ext_milli = 0;
+    o->exact_search = 0;
+    o->t2_f32 = 1;
+    o->t2_margin = 4e-5;
+    return OFDM_OK;
+}
+
+int ofdm_get_walk_tuning(const ofdm_ctx* c, ofdm_walk_tuning* o)
+{
+    if (!c || !o) return fail(OFDM_ERR_INVALID, "null argument");
+    *o = c->walk;
+    return OFDM_OK;
+}
+
+int ofdm_set_walk_tuning(ofdm_ctx* c, const ofdm_walk_tuning* t)
+{
+    if (!c || !t) return fail(OFDM_ERR_INVALID, "null argument");
+    if (t->chunks_per_slot < 1 || t->halo_milli < 0 || t->ext_milli < 0 || !(t->t2_margin >= 0.0))
+        return fail(OFDM_ERR_INVALID, "walk tuning out of range");
+    c->walk = *t;
+    return OFDM_OK;
 }
 
 int ofdm_rx_stream_shard(ofdm_ctx* c, const double* iq, const int16_t* iq16, size_t n, long start, long own_lo,

@@ -320,11 +320,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8) tx_kernel(TxArgs a)
                 z.x += w.x;
                 z.y += w.y;
             }
-#ifdef OFDM_TX_PLAIN  // timing experiment only
-            out[j] = z;
-#else
             store_nt(out + j, z);
-#endif
         };
         if (cp_reg) {
 #pragma unroll
@@ -387,11 +383,7 @@ struct SymbolRegs<LOGN, false> {
         constexpr int T = (1 << LOGN) / 8;
 #pragma unroll
         for (int i = 0; i < 8; ++i)
-#ifdef OFDM_RX_PLAIN  // timing experiment only
-            r[i] = a.iq[off + t + T * i];
-#else
             r[i] = load_nt(a.iq + off + t + T * i);
-#endif
     }
     __device__ __forceinline__ double2 get(int i) const { return r[i]; }
 };
@@ -448,11 +440,7 @@ __device__ __forceinline__ void dma_symbol(const RxArgs& a, long off, void* stag
                 "s_mov_b32 %0, m0\n\t"
                 "s_mov_b32 m0, %2\n\t"
                 "s_nop 0\n\t"
-#ifdef OFDM_RX_PLAIN
-                "global_load_lds_dwordx4 %1, off\n\t"
-#else
                 "global_load_lds_dwordx4 %1, off nt\n\t"
-#endif
                 "s_mov_b32 m0, %0"
                 : "=&s"(keep)
                 : "v"(g), "s"(lds)
@@ -499,13 +487,6 @@ __device__ __forceinline__ double2 stage_get(const void* stage, int e)
         return reinterpret_cast<const double2*>(stage)[e];
     }
 }
-
-#ifdef OFDM_RX_PROF  // timing experiment only: per-workgroup rx phase clocks (wave 0)
-__device__ unsigned long long g_rx_prof[2 * 4096 * 8];
-#define RPROF(...) __VA_ARGS__
-#else
-#define RPROF(...)
-#endif
 
 template <int LOGN, bool STAGED, bool I16, bool SYNC>
 __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
@@ -573,8 +554,6 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
     lds_barrier();  // twiddle table visible: fft_pp reads a pass's twiddles before its barrier
 
     unsigned long long errs = 0;
-    RPROF(unsigned long long p_s0 = 0, p_pf = 0, p_fft = 0, p_epi = 0, p_nf = 0, p_gain = 0, p_emit = 0, p_pack = 0;
-          const unsigned long long p_c0 = clock64(); const unsigned long long p_w0 = wall_clock64();)
 
     // Persistent over frames (grid <= 2 workgroups per CU): the next frame's
     // symbol 0 is fetched (LDS-DMA into bufB) while this frame's epilogue
@@ -609,18 +588,14 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
 #pragma unroll 1
         for (int s = 0; s < S; ++s) {
             double2 v[8];
-            RPROF(const unsigned long long p_a = clock64();)
             if (s == 0) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of symbol 0 landed
-                RPROF(p_s0 += clock64() - p_a;)
 #pragma unroll
                 for (int i = 0; i < 8; ++i) v[i] = stage_get<LOGN, I16>(bufB, t + T * i);
             } else {
-                RPROF(asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); p_pf += clock64() - p_a;)
 #pragma unroll
                 for (int i = 0; i < 8; ++i) v[i] = pf.get(i);
             }
-            RPROF(const unsigned long long p_b = clock64();)
             // SYNC: the phase ramp is applied before the next symbol's
             // prefetch is issued, so its sincos temporaries are not live
             // beside the 8 prefetch registers (which spilled at N = 512)
@@ -646,14 +621,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
             // beside the register window
             int tl;
             asm volatile("v_mov_b32 %0, %1" : "=v"(tl) : "v"(t));
-#ifdef OFDM_RX_NOFFT  // timing experiment only: the transform replaced by one LDS hand-off
-            double2* res = first;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) first[lds_swz(tl + T * i)] = v[i];
-            lds_barrier();
-#else
             double2* res = fft_pp<LOGN, -1>(v, tl, lds_tw, first, second);
-#endif
             first = res == bufA ? bufB : bufA;
             second = res;
             if (t < P) pil[s * P + t] = res[pbin];
@@ -677,9 +645,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
                     default: break;
                 }
             }
-            RPROF(p_fft += clock64() - p_b;)
         }
-        RPROF(const unsigned long long p_e = clock64();)
         lds_barrier();  // pilots of the last symbol visible; every thread is done reading bufB
         // The channel carriers go to LDS (bufA past the decisions) by DMA
         // issued ahead of the next frame's symbol 0: read per point from HBM
@@ -732,7 +698,6 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
             fnext = fstep + __builtin_amdgcn_readfirstlane(*qslot);  // uniform: an SGPR
             if (fnext < nfr) dma_symbol<LOGN, I16>(a, body0(frame_of(fnext)), bufB, t);
         }
-        RPROF(const unsigned long long p_g = clock64(); p_gain += p_g - p_e;)
 
         // One symbol's RX_DPT points of the register window. Without a
         // channel (the common case) the group's gain loads are issued first
@@ -745,10 +710,8 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
             int d = t + T * i, gi = s * P + (pk[i] >> 16);
             asm volatile("" : "+v"(d), "+v"(gi));
             double2 o = cmul_exact(yv, gain[gi]);
-#ifndef OFDM_RX_NOCHAN  // timing experiment only: no channel correction
             const double2 cv = chan_lds ? chl[d] : load_untracked(chan + d);
             o = a.chan_recip ? cmul_exact(o, cv) : cdiv_exact(o, cv);
-#endif
             if (a.constell) store_nt(a.constell + (f * S + s) * D + d, o);
             dec[whole_frame_dec ? s * D + d : d] = (uint8_t)decide(o, a.k, s1, m);
         };
@@ -763,13 +726,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
                 asm volatile("" : "+v"(d), "+v"(gi));  // opaque: not hoisted and held
                 if (d < D) {
                     const double2 o = cmul_exact(yw[i], gain[gi]);
-                    if constexpr (decltype(with_store)::value) {
-#ifdef OFDM_RX_NOCSTORE  // timing experiment only: no constellation stores
-                        if (o.x == 12345.678) store_nt(cbase + d, o);
-#else
-                        store_nt(cbase + d, o);
-#endif
-                    }
+                    if constexpr (decltype(with_store)::value) store_nt(cbase + d, o);
                     dec[whole_frame_dec ? s * D + d : d] = (uint8_t)decide_select(o, a.k, s1, m);
                 }
             }
@@ -841,14 +798,11 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
                     default: break;
                 }
             }
-            RPROF(p_emit += clock64() - p_g;)
             lds_barrier();
-            RPROF(const unsigned long long p_k = clock64();)
             if (by_word)
                 pack_words();
             else
                 pack(0, bpf, 0);
-            RPROF(p_pack += clock64() - p_k;)
         } else {
             const long bps = (long)D * a.k / 8;  // bytes per symbol (host checks D*k % 8 == 0)
             for (int s = 0; s < S; ++s) {
@@ -866,15 +820,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
             if (whole_frame_dec) pack(0, bpf, 0);
         }
         lds_barrier();  // dec / pil / gain / red are rewritten by the next frame
-        RPROF(p_epi += clock64() - p_e; ++p_nf;)
     }
-    RPROF(if (t0 == 0 && blockIdx.x < 4096) {
-        unsigned long long* q = g_rx_prof + 8 * blockIdx.x;
-        q[0] = p_s0; q[1] = p_pf; q[2] = p_fft; q[3] = p_epi; q[4] = p_nf; q[5] = clock64() - p_c0;
-        q[6] = p_w0; q[7] = wall_clock64();
-        unsigned long long* u = g_rx_prof + 8 * 4096 + 8 * blockIdx.x;
-        u[0] = p_gain; u[1] = p_emit; u[2] = p_pack;
-    })
     if (a.bit_errors) {
         errs = block_sum_u64<T>(errs, red);
         if (t0 == 0 && errs) atomicAdd(a.bit_errors, errs);
@@ -992,18 +938,8 @@ __global__ void f64_to_i16_kernel(const double2* __restrict__ in, long n, double
     }
 }
 
-#ifdef OFDM_RX_PROF
-extern "C" int ofdm_rx_prof(unsigned long long* out)
-{
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rx_prof), sizeof(unsigned long long) * 2 * 4096 * 8) == hipSuccess
-               ? 0
-               : -1;
-}
-#endif
-
 // ------------------------------------------------------------------ launchers
 static int num_cus();
-static long env_wgs_per_cu(const char* name);
 
 template <int LOGN, bool POINTS, bool NOISE, bool I16>
 static hipError_t tx_launch_n(const TxArgs& a, hipStream_t st)
@@ -1014,9 +950,7 @@ static hipError_t tx_launch_n(const TxArgs& a, hipStream_t st)
     const long nsym = a.nframes * a.S;
     if (nsym <= 0) return hipSuccess;
     // persistent grid: enough workgroups to fill every CU several times over
-    long grid = nsym < TX_MAX_GRID ? nsym : TX_MAX_GRID;
-    const long ov = env_wgs_per_cu("OFDM_TX_WGS_PER_CU");
-    if (ov > 0 && ov * num_cus() < grid) grid = ov * num_cus();
+    const long grid = nsym < TX_MAX_GRID ? nsym : TX_MAX_GRID;
     hipLaunchKernelGGL((tx_kernel<LOGN, POINTS, NOISE, I16>), dim3((unsigned)grid), dim3(FS::T), shm, st, a);
     return hipGetLastError();
 }
@@ -1061,15 +995,6 @@ static int num_cus()
     return cache[dev];
 }
 
-// Timing experiments (tools/overlap_probe.py): cap a persistent grid at this
-// many workgroups per CU, so a tx and an rx launch can share the CUs. Unset
-// or 0: the occupancy limit.
-static long env_wgs_per_cu(const char* name)
-{
-    const char* e = getenv(name);
-    return e ? atol(e) : 0;
-}
-
 template <int LOGN>
 static size_t rx_shm(const RxArgs& a)
 {
@@ -1089,9 +1014,7 @@ static hipError_t rx_launch_n(const RxArgs& a, hipStream_t st)
     // window's occupancy: 2 per SIMD), as far as LDS allows
     const long per_cu_w = RX_WAVES_PER_CU / (FS::T >= 64 ? FS::T / 64 : 1);
     const long per_cu_l = (long)(160 * 1024) / (long)shm;
-    long per_cu = per_cu_w < per_cu_l ? per_cu_w : per_cu_l;
-    const long ov = env_wgs_per_cu("OFDM_RX_WGS_PER_CU");
-    if (ov > 0 && ov < per_cu) per_cu = ov;
+    const long per_cu = per_cu_w < per_cu_l ? per_cu_w : per_cu_l;
     const long cap = per_cu * num_cus();
     const long grid = a.nframes < cap ? a.nframes : cap;
     hipLaunchKernelGGL((rx_kernel<LOGN, STAGED, I16, SYNC>), dim3((unsigned)grid), dim3(FS::T), shm, st, a);
@@ -1124,10 +1047,8 @@ static hipError_t rx_dispatch(const RxArgs& a, hipStream_t st, bool* staged)
     if (!fits && a.ystage == nullptr) return hipErrorInvalidValue;
     if (a.starts) {  // stream mode: register window only
         if (!fits || !a.corr) return hipErrorInvalidValue;
-#ifndef OFDM_RX_STREAM1  // timing experiment only: one wave per frame at N = 512
         if (LOGN == 9 && a.chan && a.chan_recip)
             return a.iq16 ? rx_stream2_launch<true>(a, st) : rx_stream2_launch<false>(a, st);
-#endif
         return a.iq16 ? rx_launch_n<LOGN, false, true, true>(a, st) : rx_launch_n<LOGN, false, false, true>(a, st);
     }
     if (a.iq16)

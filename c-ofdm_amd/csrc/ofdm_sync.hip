@@ -36,13 +36,6 @@
 #pragma clang fp contract(off)
 
 namespace ofdm {
-#ifdef OFDM_WALK_PROF  // timing experiment only: stream_params_kernel phase clocks (summed over frames)
-__device__ unsigned long long g_params_prof[16];
-#define PPROF(...) __VA_ARGS__
-#else
-#define PPROF(...)
-#endif
-
 
 namespace {
 
@@ -776,7 +769,6 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 3) stream_params_kernel(Strea
     const double cfo = a.cfo[f];
     const int L = N + a.cp, half = a.D / 2, Q = 1 + a.S, LT = L / T, CT = a.cp / T;
 
-    PPROF(unsigned long long pc0 = clock64(), pc1;)
     // The per-thread table entries are requested before the stream samples:
     // vector-memory returns are in order, so a table load issued later waits
     // behind every stream load in flight on the CU. (Doing the same for the
@@ -845,7 +837,6 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 3) stream_params_kernel(Strea
         if (two) wave_part(q + 1, acc1);
     }
     __syncthreads();
-    PPROF(pc1 = clock64(); if (t == 0) atomicAdd(&g_params_prof[0], pc1 - pc0); pc0 = pc1;)
     for (int q = t; q < Q; q += T) {
         double2 acc = make_double2(0.0, 0.0);
         for (int u = 0; u < NWV; ++u) acc = cadd(acc, part[q * NWV + u]);
@@ -853,7 +844,6 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 3) stream_params_kernel(Strea
         phi[q] = atan2(r.y, r.x);
     }
     __syncthreads();
-    PPROF(pc1 = clock64(); if (t == 0) atomicAdd(&g_params_prof[1], pc1 - pc0); pc0 = pc1;)
     if (t == 0) {
         double acc = 0.0;
         for (int q = 0; q < Q; ++q) {
@@ -920,7 +910,6 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 3) stream_params_kernel(Strea
             if (t + T * u < half) dat[t + T * u] = cmul_exact(dz[u], rot);
     }
     __syncthreads();
-    PPROF(pc1 = clock64(); if (t == 0) atomicAdd(&g_params_prof[3], pc1 - pc0); pc0 = pc1;)
     double acc = 0.0;
     for (int i = t; i < a.P; i += T) acc += hypot(pil[i].x, pil[i].y);
     acc = block_sum2<T>(make_double2(acc, 0.0), red).x;
@@ -939,14 +928,12 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 3) stream_params_kernel(Strea
     }
     __syncthreads();
     unwrap_scan<T>(ph, half, reinterpret_cast<unsigned*>(red + 24));  // one-pass unwrap (Frame.hpp:407-414)
-    PPROF(pc1 = clock64(); if (t == 0) atomicAdd(&g_params_prof[4], pc1 - pc0); pc0 = pc1;)
     double sxy = 0.0, sy = 0.0;
     for (int i = t; i < half; i += T) {
         sxy += ph[i] * i;
         sy += ph[i];
     }
     const double2 sums = block_sum2<T>(make_double2(sxy, sy), red + 16);
-    PPROF(pc1 = clock64(); if (t == 0) atomicAdd(&g_params_prof[5], pc1 - pc0); pc0 = pc1;)
     const double hn = (double)half;
     const double sx = hn * (hn - 1) / 2, sx2 = (hn - 1) * hn * (2 * hn - 1) / 6;
     const double b = (sums.x - sx * sums.y) / (sx2 - sx * sx);
@@ -964,7 +951,6 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 3) stream_params_kernel(Strea
         // constell /= chan would round it) instead of a division per point
         chan[i] = a.chan_recip ? cdiv_exact(make_double2(1.0, 0.0), make_double2(cs, sn)) : make_double2(cs, sn);
     }
-    PPROF(pc1 = clock64(); if (t == 0) atomicAdd(&g_params_prof[6], pc1 - pc0); pc0 = pc1;)
     // message symbols: theta(m) = A_s + B_s m over the CP-stripped body
     for (int s = t; s < a.S; s += T) {
         const int q = 1 + s;
@@ -978,7 +964,6 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 3) stream_params_kernel(Strea
         o[2] = cs;
         o[3] = sn;
     }
-    PPROF(pc1 = clock64(); if (t == 0) { atomicAdd(&g_params_prof[7], pc1 - pc0); atomicAdd(&g_params_prof[8], 1ULL); })
 }
 
 template <int LOGN>
@@ -1029,7 +1014,7 @@ hipError_t launch_stream_params(int logn, const StreamParamsArgs& a, hipStream_t
 // replaces (same transforms, same reduction orders), so the results are the
 // same to the last bit.
 // ========================================================================
-// LDS of the sync stage (stream_sync_kernel, stream_decode_kernel).
+// LDS of the sync stage (stream_decode_kernel).
 struct SyncLds {
     double2* tw9;   // TwLds<9>
     double2* tw7;   // TwLds<7>
@@ -1372,28 +1357,6 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
     __syncthreads();  // the outputs visible (LDS); the stage's LDS is free
 }
 
-__global__ void __launch_bounds__(128, 4) stream_sync_kernel(CfoArgs c, StreamParamsArgs a)
-{
-    extern __shared__ double2 smem[];
-    SyncLds Ls;
-    Ls.tw9 = smem;
-    Ls.tw7 = Ls.tw9 + TwLds<9>::SIZE;
-    Ls.img = Ls.tw7 + TwLds<7>::SIZE;
-    Ls.pil = Ls.img + 640;
-    Ls.dat = Ls.pil + a.P;
-    Ls.red = Ls.dat + (a.D / 2 + 1);
-    Ls.cps = Ls.red + 32;
-    Ls.amp = reinterpret_cast<double*>(Ls.img);
-    Ls.ph = reinterpret_cast<double*>(Ls.cps + 1 + a.S);
-    Ls.phi = Ls.ph + a.D / 2 + 2;
-    Ls.psi = Ls.phi + 64;
-    Ls.scal = Ls.psi + 64;
-    Ls.wsum = reinterpret_cast<int*>(Ls.scal + 4);
-    const long f = blockIdx.x;
-    if (a.count && f >= *a.count) return;  // uniform: past the speculative frame count
-    sync_frame(c, a, f, Ls, a.chan_out + f * a.D, a.corr_out + f * a.S * 4, true);
-}
-
 // ========================================================================
 // The whole fused stream decode in one kernel (N = 512, 640-point CFO form):
 // one workgroup per located frame runs sync_frame (pilot_freq_sinh, the CP / phase
@@ -1488,17 +1451,6 @@ hipError_t launch_stream_decode(const CfoArgs& c, const StreamParamsArgs& a, con
     return r.iq16 ? decode_launch<true>(c, a, r, st) : decode_launch<false>(c, a, r, st);
 }
 
-hipError_t launch_stream_sync(const CfoArgs& c, const StreamParamsArgs& a, int logn, int logm, int g, hipStream_t st)
-{
-    if (a.nframes <= 0) return hipSuccess;
-    if (!stream_sync_geometry(c, a, logn, logm, g)) return hipErrorNotSupported;  // the two-kernel path covers other geometries
-    const size_t shm = sizeof(double2) * (TwLds<9>::SIZE + TwLds<7>::SIZE + 640 + a.P + (a.D / 2 + 1) + 32 + 1 + a.S) +
-                       sizeof(double) * (a.D / 2 + 2 + 64 + 64 + 4) + sizeof(int) * (a.P + 2);
-    lds_opt_in((const void*)stream_sync_kernel, 160 * 1024);
-    hipLaunchKernelGGL(stream_sync_kernel, dim3((unsigned)a.nframes), dim3(128), shm, st, c, a);
-    return hipGetLastError();
-}
-
 // ========================================================================
 // Streaming detection walk (rx.cpp:125-221; oracle orc_stream_walk). One
 // 256-thread workgroup walks one chunk of the stream sequentially:
@@ -1514,14 +1466,6 @@ hipError_t launch_stream_sync(const CfoArgs& c, const StreamParamsArgs& a, int l
 // ========================================================================
 namespace {
 
-#ifdef OFDM_WALK_PROF  // timing experiment only: per-walker phase clocks
-__device__ unsigned long long g_walk_prof[8192 * 8];
-__device__ unsigned long long g_walk_fallbacks;
-__device__ unsigned long long g_walk_sub[8192 * 8];  // sub-phase clocks per walker
-#define WPROF(...) __VA_ARGS__
-#else
-#define WPROF(...)
-#endif
 
 // Walker workgroup: 128 threads (2 waves) for T2sin_size <= 1024, so that 8
 // walkers share a CU (~19 KB of LDS each, 128 VGPRs = 4 waves per SIMD): the
@@ -1808,7 +1752,6 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
     constexpr double U = 0x1.0p-53;
     constexpr int LM = WALK_FFT_LOGM, M = WALK_FFT_M, R = M / 64;
     static_assert(M == 512, "one wave: M/8 = 64 lanes");
-    WPROF(const unsigned long long q0 = clock64(); unsigned long long q1 = q0, q2 = q0, q3 = q0;)
     if (t < 64) {  // wave 0
         const int L = a.L, C = a.cycles, Q = M - L + 1;
         double mrun = 0.0, erun = 0.0;  // largest window sum / sample energy of the windows so far
@@ -1862,7 +1805,6 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) emax = fmax(emax, __shfl_xor(emax, o));
             fft_regs_wave<LM, -1>(v, lane, tw_m, buf);  // X[lane + 64 i] (its LDS syncs publish P too)
-            WPROF(q1 = clock64();)
             // Y = X . tspec (L2-resident table). The table address comes from
             // an opaque copy of the lane here: hoisted out of the walk loop,
             // the eight 64-bit addresses stayed live (and spilled) across it
@@ -1876,9 +1818,7 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
 #pragma unroll
                 for (int i = 0; i < 8; ++i) v[i] = cmul(v[i], ts[i]);
             }
-            WPROF(q2 = clock64();)
             fft_regs_wave<LM, +1>(v, lane, tw_m, buf);  // v[j] = M e_{i0 + lane + 64 j} (P final: synced inside)
-            WPROF(q3 = clock64();)
             // parked in LDS (each lane its own entries, after its last read of
             // the image), so the decisions below run as a rolled loop
 #pragma unroll
@@ -1925,13 +1865,7 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
     }
     lds_barrier();  // the answer visible to every wave
     const int found = *res;
-    WPROF(if (t == 0 && blockIdx.x < 8192) {
-        unsigned long long* q = g_walk_sub + 8 * blockIdx.x;
-        const unsigned long long q4 = clock64();
-        q[0] += q1 - q0; q[1] += q2 - q1; q[2] += q3 - q2; q[3] += q4 - q3;
-    })
     if (found < -1) {  // uniform: a lag within the error bounds of a threshold
-        WPROF(if (t == 0) atomicAdd(&g_walk_fallbacks, 1ULL));
         lds_barrier();  // every wave has read *res (the exact search reuses the scratch)
         return walk_preamble_exact<WT>(a, s, xs, a.templ, normv, best, t);
     }
@@ -2000,8 +1934,6 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
         bslot[3] = INT_MAX;
     }
     unsigned scan_it = 0;  // T2 scan steps so far (uniform): picks the bslot
-    WPROF(unsigned long long p_t2 = 0, p_n2 = 0, p_pre = 0, p_np = 0, p_steps = 0;
-          const unsigned long long p_w0 = wall_clock64(); const unsigned long long p_c0 = clock64();)
     // chunks: from the queue until it is drained (walkers that run slower on
     // their CU take fewer), or the workgroup's one chunk
     for (int round = 0;; ++round) {
@@ -2060,7 +1992,6 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
         // find_t2sin(pos): blocks pos + k*N, first hit wins
         long hit = -1;
         bool stop = false;
-        WPROF(++p_steps; unsigned long long p_a = clock64();)
         // FP64: G blocks from `base` (block g per group of T threads); the
         // first block whose ratio exceeds the level (Frame.hpp:150-197), or
         // INT_MAX. Slot scan_it & 1 collects the first hit; the other slot was
@@ -2145,7 +2076,6 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
                 float4* fftb32 = reinterpret_cast<float4*>(big);  // one image per group, both blocks
                 const float lev = (float)a.t2_level, marg = (float)a.t2_margin;
                 for (long base = pos;; base += 2L * G * N) {
-                    WPROF(++p_n2;)
                     if (scan_stop(base)) {
                         stop = true;
                         break;
@@ -2210,7 +2140,6 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
                     }
                     ++scan_it;
                     if (bg != INT_MAX && bu == bg) {  // uniform: this step's decision in FP64
-                        WPROF(if (t == 0) atomicAdd(&g_walk_fallbacks, 1ULL << 32));
                         bg = t2_eval64(base);
                         if (bg == INT_MAX) {
                             bg = t2_eval64(base + (long)G * N);
@@ -2226,7 +2155,6 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
         }
         if (!(T <= 64 && a.t2_f32)) {
             for (long base = pos;; base += (long)G * N) {
-                WPROF(++p_n2;)
                 if (scan_stop(base)) {
                     stop = true;
                     break;
@@ -2238,14 +2166,11 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
                 }
             }
         }
-        WPROF(unsigned long long p_b = clock64(); p_t2 += p_b - p_a;)
         if (stop) break;
-        WPROF(++p_np;)
         const int lag = (a.tspec && !a.exact_only)
                             ? walk_preamble_fft<WT>(a, hit, big, P, tw_m, reinterpret_cast<int*>(scr + 2), xs, normv,
                                                     best, t)
                             : walk_preamble<WT>(a, hit, xs, ctap, E, normv, best, unsure, mred, t);
-        WPROF(p_pre += clock64() - p_b;)
         const long pb = (lag == INT_MAX ? -10 : hit + lag) + 1;  // rx.cpp:160
         if (pb < -2) {                                            // rx.cpp:162-168
             pos = hit + a.msg;
@@ -2274,11 +2199,6 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
         }
     }
     }  // chunks
-    WPROF(if (t0 == 0 && blockIdx.x < 8192) {
-        unsigned long long* q = g_walk_prof + 8 * blockIdx.x;
-        q[0] = clock64() - p_c0; q[1] = p_t2; q[2] = p_n2; q[3] = p_pre; q[4] = p_np;
-        q[5] = p_steps; q[6] = p_w0; q[7] = wall_clock64();
-    })
 }
 
 __global__ void gather_kernel(GatherArgs a)
@@ -2467,19 +2387,3 @@ hipError_t launch_gather(const GatherArgs& a, hipStream_t st)
 
 }  // namespace ofdm
 
-#ifdef OFDM_WALK_PROF
-extern "C" int ofdm_walk_prof(unsigned long long* out, unsigned long long* fallbacks)
-{
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ofdm::g_walk_prof), sizeof(unsigned long long) * 8192 * 8) != hipSuccess)
-        return -1;
-    if (hipMemcpyFromSymbol(fallbacks, HIP_SYMBOL(ofdm::g_walk_fallbacks), sizeof(unsigned long long)) != hipSuccess)
-        return -1;
-    if (hipMemcpyFromSymbol(out + 8192 * 8, HIP_SYMBOL(ofdm::g_walk_sub), sizeof(unsigned long long) * 8192 * 8) !=
-        hipSuccess)
-        return -1;
-    if (hipMemcpyFromSymbol(out + 2 * 8192 * 8, HIP_SYMBOL(ofdm::g_params_prof), sizeof(unsigned long long) * 16) !=
-        hipSuccess)
-        return -1;
-    return 0;
-}
-#endif

@@ -112,6 +112,10 @@ struct WalkArgs {
 };
 constexpr int WALK_FFT_LOGM = 9;
 constexpr int WALK_FFT_M = 1 << WALK_FFT_LOGM;
+// Samples one T2 scan step of a walker covers at most (stream_walk_kernel:
+// the FP32 screen's 2*G blocks of T2sin_size = 2 x 128 threads x 8 samples
+// for T2sin_size <= 512; G = 1 FP64 block of up to 2048 samples above).
+constexpr long WALK_SCAN_MAX = 2048;
 
 struct GatherArgs {
     const double2* iq;
@@ -165,7 +169,6 @@ hipError_t launch_compact(const CompactArgs& a, hipStream_t st);
 hipError_t launch_stream_params(int logn, const StreamParamsArgs& a, hipStream_t st);
 // pilot_freq_sinh + the params stage fused (N = 512, 640-point CFO form);
 // hipErrorNotSupported for other geometries (use launch_cfo + launch_stream_params)
-hipError_t launch_stream_sync(const CfoArgs& c, const StreamParamsArgs& a, int logn, int logm, int g, hipStream_t st);
 // the whole fused decode (sync stage + rx stage) in one kernel for the same
 // geometries (r: the stream rx arguments; corr / chan pass through LDS)
 hipError_t launch_stream_decode(const CfoArgs& c, const StreamParamsArgs& a, const RxArgs& r, int logn, int logm, int g,

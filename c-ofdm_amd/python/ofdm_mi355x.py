@@ -54,6 +54,12 @@ class Channel(C.Structure):
     _fields_ = [("noise_std", C.c_double), ("seed", C.c_ulonglong), ("sample_offset", C.c_ulonglong)]
 
 
+class WalkTuning(C.Structure):
+    """ofdm_walk_tuning: per-context stream walker settings (tests, experiments)."""
+    _fields_ = [("chunks_per_slot", C.c_long), ("halo_milli", C.c_long), ("ext_milli", C.c_long),
+                ("exact_search", C.c_int), ("t2_f32", C.c_int), ("t2_margin", C.c_double)]
+
+
 class OfdmError(RuntimeError):
     def __init__(self, code: int, msg: str):
         super().__init__(f"ofdm error {code} ({ERRORS.get(code, '?')}): {msg}")
@@ -104,6 +110,10 @@ SIGNATURES = {
     "ofdm_rx_stream_i16": (_I, [_V, _V, _SZ, _SZ, _L, _V, _V, _V, _V, C.POINTER(_SZ), _V]),
     "ofdm_rx_stream_shard": (_I, [_V, _V, _V, _SZ, _L, _L, _L, _SZ, _L, _V, _V, _V, _V, C.POINTER(_SZ), _V, _SZ,
                                   C.POINTER(_SZ), C.POINTER(_L), _V]),
+    "ofdm_stream_shard_margins": (_I, [_V, C.POINTER(_L), C.POINTER(_L)]),
+    "ofdm_walk_tuning_default": (_I, [C.POINTER(WalkTuning)]),
+    "ofdm_get_walk_tuning": (_I, [_V, C.POINTER(WalkTuning)]),
+    "ofdm_set_walk_tuning": (_I, [_V, C.POINTER(WalkTuning)]),
 }
 
 _lib = None
@@ -310,6 +320,26 @@ class Modem:
         check(lib().ofdm_rx_stream_i16(self.h, _ptr(iq16), n, max_frames, chunk, _ptr(pb_out), _ptr(bytes_out),
                                        _ptr(constell_out), _ptr(cfo_out), C.byref(m), _stream(stream)))
         return m.value
+
+    def walk_tuning(self, **changes) -> dict:
+        """ofdm_set_walk_tuning: start from the defaults, apply `changes`
+        (WalkTuning field names); returns the previous settings as a dict."""
+        old = WalkTuning()
+        check(lib().ofdm_get_walk_tuning(self.h, C.byref(old)))
+        t = WalkTuning()
+        check(lib().ofdm_walk_tuning_default(C.byref(t)))
+        for k, v in changes.items():
+            if not hasattr(t, k):
+                raise KeyError(k)
+            setattr(t, k, v)
+        check(lib().ofdm_set_walk_tuning(self.h, C.byref(t)))
+        return {f: getattr(old, f) for f, _ in WalkTuning._fields_}
+
+    def shard_margins(self) -> tuple[int, int]:
+        """ofdm_stream_shard_margins: (halo, tail) samples a stream shard needs."""
+        h, t = C.c_long(), C.c_long()
+        check(lib().ofdm_stream_shard_margins(self.h, C.byref(h), C.byref(t)))
+        return h.value, t.value
 
     def rx_stream_shard(self, iq, n: int, start: int, own_lo: int, own_hi: int, max_frames: int, pb_out=None,
                         bytes_out=None, constell_out=None, cfo_out=None, chunk: int = 0, i16: bool = False,

@@ -34,7 +34,11 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-WALK_SCAN = 2048  # samples one walker scan step covers (256 threads x 8 samples, ofdm_sync.hip)
+# Samples one walker T2 scan step covers at most (ofdm_sync.hpp WALK_SCAN_MAX:
+# the FP32 screen's 2 x 128 threads x 8 samples). The library states what a
+# shard needs (ofdm_stream_shard_margins); tests/test_gpu_stream.py checks
+# stream_halo / stream_tail against it.
+WALK_SCAN = 2048
 
 
 def geometry(params: dict) -> dict:

@@ -327,6 +327,36 @@ int ofdm_rx_stream_shard(ofdm_ctx* ctx, const double* iq, const int16_t* iq16, s
                          size_t* nframes_out, long* located, size_t located_cap,
                          size_t* nlocated_out, long* exit_out, void* stream);
 
+/* Samples a shard of ofdm_rx_stream_shard needs around its core
+ * [own_lo, own_hi): *halo_out before own_lo for the walk-in to meet the true
+ * walk without a re-walk (the walkers' chunk halo), *tail_out past own_hi for
+ * the step that crosses own_hi (one scan step, a T2 block, the preamble
+ * window, then the frame). Either pointer may be NULL. */
+int ofdm_stream_shard_margins(const ofdm_ctx* ctx, long* halo_out, long* tail_out);
+
+/* ---- stream walk tuning (tests and experiments) --------------------------
+ * Per-context settings of the ofdm_rx_stream* walkers; ofdm_create sets the
+ * defaults (ofdm_walk_tuning_default), which are the product configuration.
+ * chunks_per_slot, halo_milli and ext_milli change only how the walk is
+ * split over walkers: the stitched walk is exact for any values (short halos
+ * cost serial re-walks). exact_search = 1 replaces the certified FFT
+ * preamble search by the reference's serial recurrence; t2_f32 = 0 turns the
+ * FP32 T2 screen off (FP64 only). t2_margin is the FP32 screen's
+ * certification margin: at or above the default 4e-5 every uncertain block is
+ * decided in FP64; a smaller margin trusts raw FP32 ratios near the level and
+ * can make the walk differ from the reference (tests use 0 and 1). */
+typedef struct ofdm_walk_tuning {
+    long chunks_per_slot; /* chunks per resident walker (>= 1; default 1)       */
+    long halo_milli;      /* walk-in halo, 1/1000 frames (default 3000)         */
+    long ext_milli;       /* walk-on past the core end, 1/1000 frames (0)       */
+    int exact_search;     /* 1: serial-recurrence preamble search (default 0)   */
+    int t2_f32;           /* 1: certified FP32 T2 screen (default 1)            */
+    double t2_margin;     /* FP32 screen margin (default 4e-5)                  */
+} ofdm_walk_tuning;
+int ofdm_walk_tuning_default(ofdm_walk_tuning* out);
+int ofdm_get_walk_tuning(const ofdm_ctx* ctx, ofdm_walk_tuning* out);
+int ofdm_set_walk_tuning(ofdm_ctx* ctx, const ofdm_walk_tuning* tuning);
+
 #ifdef __cplusplus
 }
 #endif

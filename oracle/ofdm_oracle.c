@@ -842,6 +842,20 @@ double orc_decode_frame(const ofdm_params* p, const double* region, double* cons
     return cfo;
 }
 
+/* orc_decode_frame on every located frame of a stream (frame f's region at
+ * x + pbs[f]), OpenMP over the frames: the per-frame chain is independent. */
+void orc_decode_frames(const ofdm_params* p, const double* x, const long* pbs, long nframes, double* cfo,
+                       double* constell, uint8_t* bytes, int threads)
+{
+    long npts = p->num_data_subc * p->num_symb, nb = npts * p->mod_type / 8;
+    if (threads < 1) threads = 1;
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 16)
+    for (long f = 0; f < nframes; f++) {
+        const double c = orc_decode_frame(p, x + 2 * pbs[f], constell + 2 * f * npts, bytes + f * nb);
+        if (cfo) cfo[f] = c;
+    }
+}
+
 /* The detection walk of rx.cpp:125-221 over one contiguous stream (the
  * ring-buffer refills of rx.cpp keep absolute positions, so over a stream
  * held whole they are the identity):

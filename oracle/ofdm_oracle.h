@@ -88,6 +88,8 @@ void orc_tx_batch(const ofdm_params* p, const uint8_t* bytes, long nframes, doub
 /* Located-frame decode (main.cpp:60-80) and the streaming detection walk
  * (rx.cpp:125-221) over a contiguous stream. */
 double orc_decode_frame(const ofdm_params* p, const double* region, double* constell, uint8_t* bytes);
+void orc_decode_frames(const ofdm_params* p, const double* x, const long* pbs, long nframes, double* cfo,
+                       double* constell, uint8_t* bytes, int threads);
 long orc_stream_walk(const ofdm_params* p, const double* x, long n, long* pb_out, long max);
 
 #ifdef __cplusplus

@@ -102,6 +102,7 @@ def lib():
             "orc_rx_batch": (u64, [PP, P_d, l, l, P_d, P_u8, P_u8, i]),
             "orc_tx_batch": (v, [PP, P_u8, l, P_d, l, i]),
             "orc_decode_frame": (d, [PP, P_d, P_d, P_u8]),
+            "orc_decode_frames": (v, [PP, P_d, C.POINTER(C.c_long), l, P_d, P_d, P_u8, i]),
             "orc_stream_walk": (l, [PP, P_d, l, C.POINTER(C.c_long), l]),
         }
         for name, (res, args) in sig.items():
@@ -374,6 +375,24 @@ def decode_frame(params, region: np.ndarray):
     cons = np.zeros(g["npts"], np.complex128)
     out = np.zeros(g["bytes_per_frame"], np.uint8)
     cfo = lib().orc_decode_frame(C.byref(p), _d(region), _d(cons), _u8(out))
+    return cfo, cons, out
+
+
+def decode_frames(params, x: np.ndarray, pbs, threads: int = 0):
+    """decode_frame on every located frame x[pbs[f]:...] (OpenMP over frames;
+    threads 0 = os.cpu_count()) -> (cfo (nf,), constell (nf, npts), bytes (nf, bpf))."""
+    import os
+    p = P(params)
+    g = geometry(p)
+    x = np.ascontiguousarray(x, np.complex128)
+    pbs = np.ascontiguousarray(pbs, np.int64)
+    nf = len(pbs)
+    assert nf == 0 or (pbs.min() >= 0 and pbs.max() + g["preamble_len"] + g["message_len"] <= len(x))
+    cfo = np.zeros(nf, np.float64)
+    cons = np.zeros((nf, g["npts"]), np.complex128)
+    out = np.zeros((nf, g["bytes_per_frame"]), np.uint8)
+    lib().orc_decode_frames(C.byref(p), _d(x), pbs.ctypes.data_as(C.POINTER(C.c_long)), nf, _d(cfo), _d(cons),
+                            _u8(out), threads or os.cpu_count() or 1)
     return cfo, cons, out
 
 

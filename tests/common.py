@@ -80,3 +80,56 @@ def impaired_stream(cfg, nf, seed, snr_db=20.0, cfo_max=0.004, gap_max=4096):
         parts += [fr, np.zeros(int(rng.integers(0, gap_max + 1)), np.complex128)]
     x = np.concatenate(parts)
     return O.awgn(x, 10 ** (-snr_db / 20), seed=seed), data
+
+
+def decision_thresholds(k):
+    """Modulation::demod's cell edges on each axis (modulation.cpp:53-87)."""
+    m = 1 << (k // 2)
+    s1 = (m - 1) / 2.0
+    return np.array([(j - 0.5) / s1 - 1.0 for j in range(1, m)])
+
+
+def distance_to_threshold(k, pts):
+    """Distance of each equalised point from the decision edge nearest to it
+    (BPSK: the line re + im = 0; QAM: the clamped re / im cell edges)."""
+    if k == 1:
+        return np.abs(pts.real + pts.imag)
+    th = decision_thresholds(k)
+    dre = np.min(np.abs(np.clip(pts.real, -1, 1)[..., None] - th), axis=-1)
+    dim = np.min(np.abs(np.clip(pts.imag, -1, 1)[..., None] - th), axis=-1)
+    return np.minimum(dre, dim)
+
+
+def check_stream_frames(cfg, x, pbs, got_bytes, got_cons, got_cfo=None, tol=1e-9):
+    """Every located frame of a stream against the oracle's main.cpp:60-80
+    chain on the same samples (orc_decode_frames): CFO exact, constellation
+    within `tol` relative per frame, and every byte equal, except that a
+    decision may differ where the oracle's own point lies within the rounding
+    band of its threshold (twice the largest GPU-oracle point difference of
+    the whole stream: the sync chain's transcendentals and the FFT round
+    differently). Returns a summary dict (printed by callers)."""
+    k = cfg["mod_type"]
+    g = O.geometry(cfg)
+    nf = len(pbs)
+    ocfo, ocons, obytes = O.decode_frames(cfg, x, pbs)
+    if got_cfo is not None:
+        bad = np.nonzero(got_cfo != ocfo)[0]
+        assert bad.size == 0, f"CFO differs on {bad.size} frames, first {bad[:8]}"
+    scale = np.abs(ocons).max(axis=1)
+    err = np.abs(got_cons - ocons).max(axis=1) / np.maximum(scale, 1e-300)
+    assert err.max() < tol, f"constellation rel err {err.max():.2e} on frame {int(err.argmax())}"
+    band = 2.0 * float(np.abs(got_cons - ocons).max())
+    diff_frames = np.nonzero(np.any(got_bytes != obytes, axis=1))[0]
+    flips, worst = 0, 0.0
+    for f in diff_frames:
+        bg = np.unpackbits(got_bytes[f])[:g["npts"] * k].reshape(-1, k)
+        bo = np.unpackbits(obytes[f])[:g["npts"] * k].reshape(-1, k)
+        pts = np.nonzero(np.any(bg != bo, axis=1))[0]
+        d = distance_to_threshold(k, ocons[f][pts])
+        flips += len(pts)
+        worst = max(worst, float(d.max()))
+        assert np.all(d <= band), (f"frame {f}: {len(pts)} decisions differ, farthest {d.max():.3e} "
+                                   f"from its threshold (band {band:.3e})")
+    return {"frames": nf, "max_constellation_rel_err": float(err.max()), "band": band,
+            "frames_with_flips": int(diff_frames.size), "decision_flips": flips,
+            "farthest_flip_from_threshold": worst}

@@ -3,6 +3,8 @@ ofdm_rx_stream's chunk-parallel walk must locate exactly the frames of the
 sequential walk (oracle orc_stream_walk) and decode each as main.cpp:60-80
 (oracle orc_decode_frame) — on the reference capture data/data.bin and on
 synthetic impaired streams, for any chunking of the walk."""
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -36,8 +38,14 @@ def host(t):
 GD = golden()
 
 
-def run_stream(cfg, x, max_frames=4096, chunk=0):
+def run_stream(cfg, x, max_frames=4096, chunk=0, tuning=None):
     m = modem(cfg)
+    if tuning:
+        old = m.walk_tuning(**tuning)
+        try:
+            return run_stream(cfg, x, max_frames, chunk)
+        finally:
+            m.walk_tuning(**old)
     g = O.geometry(cfg)
     dx = dev(x)
     pbs = torch.full((max_frames,), -1, dtype=torch.int64, device="cuda")
@@ -84,42 +92,35 @@ def test_stream_config4_matches_sequential_walk(chunk):
 
 @pytest.mark.parametrize("halo,ext", [(0, 0), (100, 0), (250, 0), (500, 0), (100, 2000), (1500, 2000)])
 @pytest.mark.parametrize("chunk", [0, 9000, 20000])
-def test_stream_short_halo_rewalks_match_sequential_walk(monkeypatch, halo, ext, chunk):
+def test_stream_short_halo_rewalks_match_sequential_walk(halo, ext, chunk):
     # walk-in halos (in 1/1000 frames) too short to meet the true walk force
     # re-walks from the previous chunk's hand-over state (with or without the
     # walk-on past the core end): still exact
-    monkeypatch.setenv("OFDM_WALK_HALO", str(halo))
-    monkeypatch.setenv("OFDM_WALK_EXT", str(ext))
     x, data = impaired_stream(D, 40, seed=4)
-    check_against_oracle(D, x, run_stream(D, x, chunk=chunk))
+    check_against_oracle(D, x, run_stream(D, x, chunk=chunk, tuning=dict(halo_milli=halo, ext_milli=ext)))
 
 
-def test_stream_walk_certified_search_equals_serial_recurrence(monkeypatch):
+def test_stream_walk_certified_search_equals_serial_recurrence():
     # the walker's parallel preamble search (window sums + error bound) against
-    # the reference's serial running-energy recurrence, forced by the test hook
+    # the reference's serial running-energy recurrence (ofdm_walk_tuning)
     x, data = impaired_stream(D, 40, seed=4)
     fast = run_stream(D, x, chunk=9000)
-    monkeypatch.setenv("OFDM_WALK_EXACT", "1")
-    exact = run_stream(D, x, chunk=9000)
+    exact = run_stream(D, x, chunk=9000, tuning=dict(exact_search=1))
     assert fast[0] == exact[0]
     for a, b in zip(fast[1:], exact[1:]):
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("env", [{"OFDM_WALK_T2_MARGIN": "1"}, {"OFDM_WALK_T2_F32": "0"}, {"OFDM_WALK_T2_MARGIN": "0"}])
-def test_stream_walk_fp32_t2_screen_equals_fp64(monkeypatch, env):
+@pytest.mark.parametrize("tuning", [dict(t2_margin=1.0), dict(t2_f32=0), dict(t2_margin=0.0)])
+def test_stream_walk_fp32_t2_screen_equals_fp64(tuning):
     # the walker's certified FP32 T2 screen against FP64 only: margin 1 makes
     # every block uncertain (each scan step re-evaluated by the FP64 path),
-    # OFDM_WALK_T2_F32=0 is the FP64 scan, margin 0 trusts the raw FP32
-    # ratios (still equal on this stream: no block within 1e-5 of the level)
+    # t2_f32 = 0 is the FP64 scan, margin 0 trusts the raw FP32 ratios
+    # (still equal on this stream: no block within 1e-5 of the level)
     for cfg, nf, seed in ((D, 40, 4), (dict(D, fft_size=256, num_data_subc=128, num_pilot_subc=8, cp_size=64), 30, 6)):
         x, data = impaired_stream(cfg, nf, seed=seed)
         screened = run_stream(cfg, x, chunk=9000)
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        other = run_stream(cfg, x, chunk=9000)
-        for k in env:
-            monkeypatch.delenv(k)
+        other = run_stream(cfg, x, chunk=9000, tuning=tuning)
         assert screened[0] == other[0]
         for a, b in zip(screened[1:], other[1:]):
             assert np.array_equal(a, b)
@@ -225,3 +226,26 @@ def test_rx_i16_equals_rx_on_converted_samples(name, cfg):
     assert outs[0][2] == 0 and np.array_equal(outs[0][1], data)
     ocons, oout, _ = O.rx_batch(cfg, host(conv), nf, g["message_len"])
     assert rel_err(outs[0][0], ocons) < 1e-9 and np.array_equal(outs[0][1], oout)
+
+
+def test_walk_tuning_defaults_and_validation():
+    m = modem(D)
+    t = M.WalkTuning()
+    M.check(M.lib().ofdm_get_walk_tuning(m.h, C.byref(t)))
+    assert (t.chunks_per_slot, t.halo_milli, t.ext_milli, t.exact_search, t.t2_f32) == (1, 3000, 0, 0, 1)
+    assert t.t2_margin == 4e-5
+    with pytest.raises(M.OfdmError):
+        m.walk_tuning(chunks_per_slot=0)
+    with pytest.raises(M.OfdmError):
+        m.walk_tuning(t2_margin=-1.0)
+    m.walk_tuning()  # back to the defaults
+
+
+def test_stream_shard_margins_cover_python_sharding():
+    # the Python shard planner (ofdm_stream.stream_halo/stream_tail) holds at
+    # least what the library says a shard needs
+    import ofdm_stream as SS
+    for cfg in (D, B, G):
+        halo, tail = modem(cfg).shard_margins()
+        assert SS.stream_halo(cfg) >= halo
+        assert SS.stream_tail(cfg) >= tail

@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from common import D, impaired_stream, rel_err
+from common import D, check_stream_frames, impaired_stream, rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -111,7 +111,8 @@ def test_sharded_stream_more_shards_than_frames():
 def test_sharded_stream_bench_size_matches_oracle(world):
     """The bench's config-4 stream (ofdm_synth, 16 384 frames, ~132 M samples)
     split over 2/4/8 contexts: every owned index equals the oracle's sequential
-    walk over the whole stream; a sample of frames decodes as the oracle."""
+    walk over the whole stream; every owned frame decodes as the oracle's
+    main.cpp:60-80 chain (common.check_stream_frames)."""
     cfg = dict(O.DEFAULT)
     lay = Y.StreamLayout(cfg, 16384)
     m = M.Modem(cfg, 0)
@@ -122,8 +123,10 @@ def test_sharded_stream_bench_size_matches_oracle(world):
     got = run_sharded(cfg, x, lay.n, world, max_frames=None)
     k = len(want)
     assert k > 0.95 * 16384
-    pick = np.unique(np.concatenate([[0, k - 1], np.random.default_rng(world).integers(0, k, 40)]))
-    check_frames(cfg, h, want, got, pick=pick)
+    pbs, byt, cons, cfo, _ = got
+    assert np.array_equal(pbs, want)
+    summary = check_stream_frames(cfg, h, pbs, byt, cons, cfo)
+    print(f"{world} shards: {summary}")
 
 
 _WALK = {}

@@ -6,7 +6,7 @@ reference's data/*.bin + data.txt: one BPSK main.cpp run, main.cpp:74-78,106-108
 import numpy as np
 
 import oracle as O
-from common import G, golden, rel_err
+from common import G, golden, impaired_stream, rel_err
 
 GD = golden()
 
@@ -105,3 +105,17 @@ def test_awgn_is_counter_based_and_thread_independent():
     c = O.awgn(x[:1000], 0.5, seed=17, sample_offset=(1 << 32) - 50000 + 777)
     assert np.array_equal(c, a[777:1777])
     assert abs(np.mean(np.abs(a) ** 2) - 0.25) < 0.01
+
+
+def test_decode_frames_batch_equals_single_frame_decode():
+    # the batched (OpenMP) orc_decode_frames used by the full-stream GPU parity
+    # tests is orc_decode_frame frame by frame
+    x, _ = impaired_stream(O.DEFAULT, 12, seed=11)
+    pbs = O.stream_walk(O.DEFAULT, x)
+    assert len(pbs) >= 8
+    cfo, cons, out = O.decode_frames(O.DEFAULT, x, pbs, threads=4)
+    g = O.geometry(O.DEFAULT)
+    span = g["preamble_len"] + g["message_len"]
+    for f, pb in enumerate(pbs):
+        c1, cons1, out1 = O.decode_frame(O.DEFAULT, x[pb:pb + span])
+        assert cfo[f] == c1 and np.array_equal(cons[f], cons1) and np.array_equal(out[f], out1)

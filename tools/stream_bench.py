@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--i16", action="store_true", help="wire-format complex<int16> stream (x mult)")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="contexts alternating on their own HIP streams (call k+1's walk overlaps call k's decode)")
+    ap.add_argument("--walk-tuning", default="",
+                    help="ofdm_set_walk_tuning fields, e.g. 'chunks_per_slot=2,halo_milli=1500,ext_milli=2000'")
     ap.add_argument("--cpu-seconds", type=float, default=0.0,
                     help="also time the oracle's walk + decode on a prefix of the stream (~this many s)")
     args = ap.parse_args()
@@ -43,6 +45,9 @@ def main():
     cfg = dict(O.DEFAULT)
     g = O.geometry(cfg)
     m = M.Modem(cfg, 0)
+    if args.walk_tuning:
+        kv = dict(item.split("=") for item in args.walk_tuning.split(","))
+        m.walk_tuning(**{k: (float(v) if k == "t2_margin" else int(v)) for k, v in kv.items()})
     nf, flen = args.frames, g["frame_len"]
     gen = torch.Generator(device="cuda").manual_seed(4)
     data = torch.randint(0, 256, (nf * g["bytes_per_frame"],), dtype=torch.uint8, device="cuda", generator=gen)

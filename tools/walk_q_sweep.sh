@@ -8,7 +8,7 @@ export OFDM_STREAM_DEBUG=1
 for cfg in ${SWEEP:-1:3000:2000 1:1500:2000 2:1500:2000}; do  # Q:halo:ext
   set -- ${cfg//:/ }
   for r in 1 2; do
-    OFDM_WALK_Q=$1 OFDM_WALK_HALO=$2 OFDM_WALK_EXT=$3 timeout -k 10 120 python tools/stream_bench.py --reps 5 > gpurun_out/wq.json 2> gpurun_out/wq.err || exit 1
+    timeout -k 10 120 python tools/stream_bench.py --reps 5 --walk-tuning chunks_per_slot=$1,halo_milli=$2,ext_milli=$3 > gpurun_out/wq.json 2> gpurun_out/wq.err || exit 1
     echo "Q=$1 halo=$2 ext=$3 $(tail -1 gpurun_out/wq.err) $(python3 -c "import json;d=json.load(open('gpurun_out/wq.json'));print(d['ms'],d['G_stream_samples_per_s'])")" >> gpurun_out/walk_q_sweep.txt
   done
 done
