@@ -2,9 +2,10 @@
 // (FFT_FORM, T2SIN_FORM, OFDM_FORM, PREAMBLE_FORM, FRAME_FORM).
 // Same class/member names, buffer ownership and in-place semantics, so
 // main.cpp / tx.cpp / rx.cpp build unchanged; every DSP member runs on the GPU
-// through the C-ABI of include/ofdm_mi355x.h (the forms stage their host
-// buffers to the device and back on each call; the batched device-pointer
-// C-ABI is the throughput path).
+// through the C-ABI of include/ofdm_mi355x.h. A FRAME_FORM keeps device
+// images of its buffers (ofdm_compat::Mirror): the forms' members move only
+// what the host changed and copy back what they change in place; the batched
+// device-pointer C-ABI is the throughput path.
 #pragma once
 #include <math.h>
 #include <stdlib.h>
@@ -29,6 +30,7 @@ const complex_double REAL_ONE(1.0, 0.0);
 
 namespace ofdm_compat {
 struct Context;
+struct FrameMirrors;
 }
 
 class FFT_FORM {
@@ -167,4 +169,6 @@ public:
     complex_vector get();                                        // Frame.cpp:244-246
     complex16_vector get_int16();                                // Frame.cpp:249-256
     void form_int16_to_double();                                 // Frame.hpp:472-481
+
+    std::shared_ptr<ofdm_compat::FrameMirrors> mirrors_;  // device images of buf / from_sdr_buf / from_sdr_int16_buf
 };

@@ -1,12 +1,20 @@
 // Frame.cpp — the FFT_FORM / T2SIN_FORM / OFDM_FORM / PREAMBLE_FORM /
-// FRAME_FORM members of the compatibility layer. Each DSP member stages its
-// host buffers to the device, runs the C-ABI entry (HIP kernels) and copies
-// the result back with the reference's in-place semantics.
+// FRAME_FORM members of the compatibility layer. Each DSP member runs its
+// C-ABI entry (HIP kernels) on its thread's compat stream, on the device
+// image of its host buffers:
+//   - a FRAME_FORM's buf, from_sdr_buf and from_sdr_int16_buf are mirrored
+//     on the device (ofdm_compat::Mirror): a member uploads only what the
+//     host changed since the last transfer and copies back what it changed
+//     in place, so rx.cpp's per-frame chain moves one frame over PCIe once;
+//   - any other host buffer is staged through the pinned arena.
+// Every member returns with its results in the host buffers, as the
+// reference's do.
 #include "OFDM/Frame.hpp"
 
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 #include "ofdm_compat.hpp"
 
@@ -34,6 +42,42 @@ ofdm_params form_params(ConfigMap& config, int num_symb, int mod)
     p.num_symb = num_symb;
     p.mod_type = mod;
     return p;
+}
+
+// The device image of the host range [h, h + n): a mirror's (made current
+// with the host) or a staged copy in scratch slot `slot`.
+struct DevRange {
+    void* d;
+    ofdm_compat::Mirror* m;
+    void* h;
+    size_t n;
+};
+
+DevRange stage_in(Context& ctx, int slot, const void* h, size_t n)
+{
+    if (ofdm_compat::Mirror* m = ofdm_compat::find_mirror(h, n)) {
+        m->push(h, n);
+        return {m->device(h), m, const_cast<void*>(h), n};
+    }
+    void* d = ctx.buf(slot, std::max<size_t>(n, 1));
+    ctx.h2d(d, h, n);
+    return {d, nullptr, const_cast<void*>(h), n};
+}
+
+// A device range the kernel is about to overwrite entirely: no upload.
+DevRange stage_out_only(Context& ctx, int slot, void* h, size_t n)
+{
+    if (ofdm_compat::Mirror* m = ofdm_compat::find_mirror(h, n)) return {m->device(h), m, h, n};
+    return {ctx.buf(slot, std::max<size_t>(n, 1)), nullptr, h, n};
+}
+
+// The host range takes the device's (after an in-place device operation).
+void stage_back(Context& ctx, const DevRange& r)
+{
+    if (r.m)
+        r.m->pull(r.h, r.n);
+    else
+        ctx.d2h(r.h, r.d, r.n);
 }
 
 }  // namespace
@@ -89,21 +133,19 @@ void FFT_FORM::write(complex_vector& input)
     const size_t np = (size_t)num_data_subc * num_symb;
     complex_vector pts(np, 0);
     std::copy_n(input.begin(), std::min(np, input.size()), pts.begin());
-    void* din = ctx_->buf(0, np * CD);
-    void* dout = ctx_->buf(1, FFT_buf.size() * CD);
-    ctx_->h2d(din, pts.data(), np * CD);
-    check(ofdm_fft_write(ctx_->ctx, (const double*)din, 1, (double*)dout, nullptr), "ofdm_fft_write");
-    ctx_->d2h(FFT_buf.data(), dout, FFT_buf.size() * CD);
+    const DevRange in = stage_in(*ctx_, 0, pts.data(), np * CD);
+    const DevRange out = stage_out_only(*ctx_, 1, FFT_buf.data(), FFT_buf.size() * CD);
+    check(ofdm_fft_write(ctx_->ctx, (const double*)in.d, 1, (double*)out.d, ctx_->stream()), "ofdm_fft_write");
+    stage_back(*ctx_, out);
 }
 
 complex_vector& FFT_FORM::read()
 {
     COMPAT_TRACE("FFT_FORM::read");
-    void* din = ctx_->buf(0, FFT_buf.size() * CD);
-    void* dout = ctx_->buf(1, restored_buf.size() * CD);
-    ctx_->h2d(din, FFT_buf.data(), FFT_buf.size() * CD);
-    check(ofdm_fft_read(ctx_->ctx, (const double*)din, 1, (double*)dout, nullptr), "ofdm_fft_read");
-    ctx_->d2h(restored_buf.data(), dout, restored_buf.size() * CD);
+    const DevRange in = stage_in(*ctx_, 0, FFT_buf.data(), FFT_buf.size() * CD);
+    const DevRange out = stage_out_only(*ctx_, 1, restored_buf.data(), restored_buf.size() * CD);
+    check(ofdm_fft_read(ctx_->ctx, (const double*)in.d, 1, (double*)out.d, ctx_->stream()), "ofdm_fft_read");
+    stage_back(*ctx_, out);
     return restored_buf;
 }
 
@@ -143,10 +185,9 @@ std::vector<double> T2SIN_FORM::corr(complex_vector& signal)
     const size_t n = signal.size();
     std::vector<double> out(size ? n / size : 0, 0.0);
     if (out.empty()) return out;
-    void* dx = ctx_->buf(0, n * CD);
+    const DevRange x = stage_in(*ctx_, 0, signal.data(), n * CD);
     void* dr = ctx_->buf(1, out.size() * sizeof(double));
-    ctx_->h2d(dx, signal.data(), n * CD);
-    check(ofdm_t2_scan(ctx_->ctx, (const double*)dx, n, 0, (double*)dr, nullptr, nullptr), "ofdm_t2_scan");
+    check(ofdm_t2_scan(ctx_->ctx, (const double*)x.d, n, 0, (double*)dr, nullptr, ctx_->stream()), "ofdm_t2_scan");
     ctx_->d2h(out.data(), dr, out.size() * sizeof(double));
     return out;
 }
@@ -156,10 +197,10 @@ int T2SIN_FORM::find_t2sin(complex_vector& signal, int start_index)
     COMPAT_TRACE("T2SIN_FORM::find_t2sin");
     // Frame.hpp:150-197 tests the blocks start + b*size in order and returns
     // the first above the level; each block's decision reads only its own
-    // samples. So the ring goes up in windows of whole blocks from
-    // start_index (a frame or two first, then doubling) and the scan stops
-    // at the first window with a hit: rx.cpp's per-frame call moves a few
-    // frames' samples over PCIe instead of the whole ring.
+    // samples. So the scan runs over windows of whole blocks from
+    // start_index (a frame or two first, then doubling) and stops at the
+    // first window with a hit: only the samples it reads are made current on
+    // the device (from_sdr_buf's mirror: normally already there).
     const long n = (long)signal.size();
     if (size <= 0 || start_index < 0 || start_index > n) return -1;
     const long nblocks = (n - start_index) / size;
@@ -168,9 +209,8 @@ int T2SIN_FORM::find_t2sin(complex_vector& signal, int start_index)
     while (b0 < nblocks) {
         const long nb = std::min(w, nblocks - b0);
         const size_t len = (size_t)nb * size;
-        void* dx = ctx_->buf(0, len * CD);
-        ctx_->h2d(dx, signal.data() + start_index + b0 * size, len * CD);
-        check(ofdm_t2_scan(ctx_->ctx, (const double*)dx, len, 0, nullptr, df, nullptr), "ofdm_t2_scan");
+        const DevRange x = stage_in(*ctx_, 0, signal.data() + start_index + b0 * size, len * CD);
+        check(ofdm_t2_scan(ctx_->ctx, (const double*)x.d, len, 0, nullptr, df, ctx_->stream()), "ofdm_t2_scan");
         int first = -1;
         ctx_->d2h(&first, df, sizeof(int));
         if (first >= 0) return (int)(start_index + b0 * size + first);
@@ -218,12 +258,12 @@ void OFDM_FORM::write(bit_vector& input)
     const size_t nb = (size_t)ctx_->geo.bytes_per_frame;
     bit_vector bytes(nb, 0);
     std::copy_n(input.begin(), std::min(nb, input.size()), bytes.begin());
-    void* db = ctx_->buf(0, nb);
-    void* dx = ctx_->buf(1, (size_t)size * CD);
-    ctx_->h2d(db, bytes.data(), nb);
-    check(ofdm_tx_modulate(ctx_->ctx, (const uint8_t*)db, 1, (double*)dx, (size_t)size, nullptr, nullptr, nullptr),
+    const DevRange b = stage_in(*ctx_, 0, bytes.data(), nb);
+    const DevRange x = stage_out_only(*ctx_, 1, output[0], (size_t)size * CD);
+    check(ofdm_tx_modulate(ctx_->ctx, (const uint8_t*)b.d, 1, (double*)x.d, (size_t)size, nullptr, nullptr,
+                           ctx_->stream()),
           "ofdm_tx_modulate");
-    ctx_->d2h(output[0], dx, (size_t)size * CD);
+    stage_back(*ctx_, x);
 }
 
 bit_vector OFDM_FORM::read()
@@ -231,11 +271,10 @@ bit_vector OFDM_FORM::read()
     COMPAT_TRACE("OFDM_FORM::read");
     const size_t nb = ((size_t)usefull_size * modType + 7) / 8;
     bit_vector out(nb);
-    void* dx = ctx_->buf(1, (size_t)size * CD);
+    const DevRange x = stage_in(*ctx_, 1, output[0], (size_t)size * CD);
     void* db = ctx_->buf(0, nb);
-    ctx_->h2d(dx, output[0], (size_t)size * CD);
-    check(ofdm_rx_demod(ctx_->ctx, (const double*)dx, 1, (size_t)size, nullptr, 0, nullptr, (uint8_t*)db, nullptr,
-                        nullptr, nullptr),
+    check(ofdm_rx_demod(ctx_->ctx, (const double*)x.d, 1, (size_t)size, nullptr, 0, nullptr, (uint8_t*)db, nullptr,
+                        nullptr, ctx_->stream()),
           "ofdm_rx_demod");
     ctx_->d2h(out.data(), db, nb);
     return out;
@@ -245,11 +284,10 @@ complex_vector OFDM_FORM::fft()
 {
     COMPAT_TRACE("OFDM_FORM::fft");
     const size_t np = (size_t)usefull_size;
-    void* dx = ctx_->buf(1, (size_t)size * CD);
+    const DevRange x = stage_in(*ctx_, 1, output[0], (size_t)size * CD);
     void* dc = ctx_->buf(2, np * CD);
-    ctx_->h2d(dx, output[0], (size_t)size * CD);
-    check(ofdm_rx_demod(ctx_->ctx, (const double*)dx, 1, (size_t)size, nullptr, 0, (double*)dc, nullptr, nullptr,
-                        nullptr, nullptr),
+    check(ofdm_rx_demod(ctx_->ctx, (const double*)x.d, 1, (size_t)size, nullptr, 0, (double*)dc, nullptr, nullptr,
+                        nullptr, ctx_->stream()),
           "ofdm_rx_demod");
     ctx_->d2h(fft_task.restored_buf.data(), dc, np * CD);
     return fft_task.restored_buf;
@@ -258,32 +296,38 @@ complex_vector OFDM_FORM::fft()
 void OFDM_FORM::cp_freq_sinh()
 {
     COMPAT_TRACE("OFDM_FORM::cp_freq_sinh");
-    void* dx = ctx_->buf(1, (size_t)size * CD);
-    ctx_->h2d(dx, output[0], (size_t)size * CD);
-    check(ofdm_cp_sync(ctx_->ctx, (double*)dx, 1, (size_t)size, num_symb, nullptr), "ofdm_cp_sync");
-    ctx_->d2h(output[0], dx, (size_t)size * CD);
+    const DevRange x = stage_in(*ctx_, 1, output[0], (size_t)size * CD);
+    check(ofdm_cp_sync(ctx_->ctx, (double*)x.d, 1, (size_t)size, num_symb, ctx_->stream()), "ofdm_cp_sync");
+    stage_back(*ctx_, x);
 }
 
 void OFDM_FORM::pr_phase_sinh(complex_double* pr, int pr_size)
 {
     COMPAT_TRACE("OFDM_FORM::pr_phase_sinh");
-    void* dx = ctx_->buf(1, (size_t)size * CD);
-    void* dp = ctx_->buf(3, (size_t)pr_size * CD);
-    ctx_->h2d(dx, output[0], (size_t)size * CD);
-    ctx_->h2d(dp, pr, (size_t)pr_size * CD);
-    check(ofdm_phase_sync(ctx_->ctx, (double*)dx, 1, (size_t)size, (size_t)size, (const double*)dp, (size_t)pr_size,
-                          nullptr),
+    const DevRange x = stage_in(*ctx_, 1, output[0], (size_t)size * CD);
+    // the caller's preamble copy (main.cpp:63 / rx.cpp:208 pass
+    // preamble.ofdm_preamble): when it holds the context's own ofdm_preamble,
+    // the device copy made at construction is used
+    const double* dp = nullptr;
+    size_t plen = (size_t)pr_size;
+    if (plen == ctx_->ofdm_preamble.size() &&
+        std::memcmp(pr, ctx_->ofdm_preamble.data(), plen * CD) == 0) {
+        plen = 0;  // ofdm_phase_sync: the context preamble
+    } else {
+        const DevRange p = stage_in(*ctx_, 3, pr, plen * CD);
+        dp = (const double*)p.d;
+    }
+    check(ofdm_phase_sync(ctx_->ctx, (double*)x.d, 1, (size_t)size, (size_t)size, dp, plen, ctx_->stream()),
           "ofdm_phase_sync");
-    ctx_->d2h(output[0], dx, (size_t)size * CD);
+    stage_back(*ctx_, x);
 }
 
 double OFDM_FORM::pilot_freq_sinh()
 {
     COMPAT_TRACE("OFDM_FORM::pilot_freq_sinh");
-    void* dx = ctx_->buf(1, (size_t)size * CD);
+    const DevRange x = stage_in(*ctx_, 1, output[0], (size_t)size * CD);
     void* dc = ctx_->buf(4, sizeof(double));
-    ctx_->h2d(dx, output[0], (size_t)size * CD);
-    check(ofdm_cfo_estimate(ctx_->ctx, (const double*)dx, 1, (size_t)size, num_symb, (double*)dc, nullptr),
+    check(ofdm_cfo_estimate(ctx_->ctx, (const double*)x.d, 1, (size_t)size, num_symb, (double*)dc, ctx_->stream()),
           "ofdm_cfo_estimate");
     double shift = 0;
     ctx_->d2h(&shift, dc, sizeof(double));
@@ -293,13 +337,12 @@ double OFDM_FORM::pilot_freq_sinh()
 void OFDM_FORM::freq_shift(double& shift)
 {
     COMPAT_TRACE("OFDM_FORM::freq_shift");
-    void* dx = ctx_->buf(1, (size_t)size * CD);
+    const DevRange x = stage_in(*ctx_, 1, output[0], (size_t)size * CD);
     void* dc = ctx_->buf(4, sizeof(double));
-    ctx_->h2d(dx, output[0], (size_t)size * CD);
     ctx_->h2d(dc, &shift, sizeof(double));
-    check(ofdm_freq_shift(ctx_->ctx, (double*)dx, 1, (size_t)size, (size_t)size, (const double*)dc, nullptr),
+    check(ofdm_freq_shift(ctx_->ctx, (double*)x.d, 1, (size_t)size, (size_t)size, (const double*)dc, ctx_->stream()),
           "ofdm_freq_shift");
-    ctx_->d2h(output[0], dx, (size_t)size * CD);
+    stage_back(*ctx_, x);
 }
 
 // ---------------------------------------------------------------- PREAMBLE_FORM
@@ -333,10 +376,10 @@ void PREAMBLE_FORM::find_corr(complex_vector& input, int start)
 {
     COMPAT_TRACE("PREAMBLE_FORM::find_corr");
     const size_t n = input.size();
-    void* dx = ctx_->buf(5, n * CD);
+    const DevRange x = stage_in(*ctx_, 5, input.data(), n * CD);
     void* dc = ctx_->buf(6, cor.size() * sizeof(double));
-    ctx_->h2d(dx, input.data(), n * CD);
-    check(ofdm_preamble_corr(ctx_->ctx, (const double*)dx, n, start, (double*)dc, nullptr), "ofdm_preamble_corr");
+    check(ofdm_preamble_corr(ctx_->ctx, (const double*)x.d, n, start, (double*)dc, ctx_->stream()),
+          "ofdm_preamble_corr");
     ctx_->d2h(cor.data(), dc, cor.size() * sizeof(double));
 }
 
@@ -344,17 +387,17 @@ int PREAMBLE_FORM::find_preamble(complex_vector& input, int start)
 {
     COMPAT_TRACE("PREAMBLE_FORM::find_preamble");
     // Frame.cpp:338-378 reads input[start .. start + cor.size() + pr_sin_len):
-    // only that window goes to the device (samples past the vector's end
-    // read as zero in the kernel, as before)
+    // only that window is made current on the device (samples past the
+    // vector's end read as zero in the kernel, as before)
     const long n = (long)input.size();
     if (start < 0 || start >= n) return -10;
     const long win = std::min<long>(n - start, (long)cor.size() + pr_sin_len);
-    void* dx = ctx_->buf(5, (size_t)win * CD);
+    const DevRange x = stage_in(*ctx_, 5, input.data() + start, (size_t)win * CD);
     int* ds = (int*)ctx_->buf(7, 2 * sizeof(int));
     const int zero = 0;
-    ctx_->h2d(dx, input.data() + start, (size_t)win * CD);
     ctx_->h2d(ds, &zero, sizeof(int));
-    check(ofdm_find_preamble(ctx_->ctx, (const double*)dx, (size_t)win, ds, 1, ds + 1, nullptr), "ofdm_find_preamble");
+    check(ofdm_find_preamble(ctx_->ctx, (const double*)x.d, (size_t)win, ds, 1, ds + 1, ctx_->stream()),
+          "ofdm_find_preamble");
     int idx = -10;
     ctx_->d2h(&idx, ds + 1, sizeof(int));
     return idx < 0 ? idx : idx + start;
@@ -363,25 +406,9 @@ int PREAMBLE_FORM::find_preamble(complex_vector& input, int start)
 complex_vector PREAMBLE_FORM::chan_char()
 {
     COMPAT_TRACE("PREAMBLE_FORM::chan_char");
-    // the averaging estimator (Frame.hpp:375-385), unused by the apps. One
-    // preamble symbol (the reference's config): pr / mod_preamble is
-    // FFT_FORM::read with mod_preamble as the caller-side divisor, which
-    // ofdm_rx_demod applies (same complex division), and the average over one
-    // symbol divides by (1, 0), an identity: all on the GPU.
-    if (num_symb == 1) {
-        void* dx = ctx_->buf(1, (size_t)size * CD);
-        void* dm = ctx_->buf(3, (size_t)num_data_subc * CD);
-        void* dc = ctx_->buf(2, (size_t)num_data_subc * CD);
-        ctx_->h2d(dx, output[0], (size_t)size * CD);
-        ctx_->h2d(dm, mod_preamble.data(), (size_t)num_data_subc * CD);
-        check(ofdm_rx_demod(ctx_->ctx, (const double*)dx, 1, (size_t)size, (const double*)dm, 0, (double*)dc, nullptr,
-                            nullptr, nullptr, nullptr),
-              "ofdm_rx_demod");
-        ctx_->d2h(chan_est.data(), dc, (size_t)num_data_subc * CD);
-        return chan_est;
-    }
-    // several preamble symbols: FFT_FORM::read on the GPU (fft()), then the
-    // caller-side per-carrier division and average, as the reference's caller code
+    // the averaging estimator (Frame.hpp:375-385), unused by the apps:
+    // FFT_FORM::read on the GPU (fft()), then the caller-side per-carrier
+    // division and the average, written as the reference writes them
     complex_vector pr = fft();
     std::fill(chan_est.begin(), chan_est.end(), complex_double(0.0, 0.0));
     for (int i = 0; i < num_data_subc * num_symb; i++) chan_est[i % num_data_subc] += pr[i] / mod_preamble[i];
@@ -392,10 +419,10 @@ complex_vector PREAMBLE_FORM::chan_char()
 complex_vector& PREAMBLE_FORM::chan_char_lq()
 {
     COMPAT_TRACE("PREAMBLE_FORM::chan_char_lq");
-    void* dx = ctx_->buf(1, (size_t)size * CD);
+    const DevRange x = stage_in(*ctx_, 1, output[0], (size_t)size * CD);
     void* dc = ctx_->buf(2, chan_est.size() * CD);
-    ctx_->h2d(dx, output[0], (size_t)size * CD);
-    check(ofdm_chan_estimate(ctx_->ctx, (const double*)dx, 1, (size_t)size, (double*)dc, chan_est.size(), nullptr),
+    check(ofdm_chan_estimate(ctx_->ctx, (const double*)x.d, 1, (size_t)size, (double*)dc, chan_est.size(),
+                             ctx_->stream()),
           "ofdm_chan_estimate");
     ctx_->d2h(chan_est.data(), dc, chan_est.size() * CD);
     return chan_est;
@@ -417,6 +444,11 @@ FRAME_FORM::FRAME_FORM(const std::string& CONFIGNAME)
       bit_preambple(usefull_size, 0)
 {
     COMPAT_TRACE("FRAME_FORM::FRAME_FORM");
+    // the device images of the frame buffer and the rx ring (f64 and int16)
+    mirrors_ = std::make_shared<ofdm_compat::FrameMirrors>();
+    mirrors_->add(message.ctx_, buf.data(), buf.size() * CD);
+    mirrors_->add(message.ctx_, from_sdr_buf.data(), from_sdr_buf.size() * CD);
+    mirrors_->add(message.ctx_, from_sdr_int16_buf.data(), from_sdr_int16_buf.size() * sizeof(std::complex<int16_t>));
     t2sin.set(buf.data());
     preamble.set(buf.data() + t2sin.size);
     message.set(buf.data() + t2sin.size + preamble.size);
@@ -438,10 +470,10 @@ complex16_vector FRAME_FORM::get_int16()
 {
     COMPAT_TRACE("FRAME_FORM::get_int16");
     auto& ctx = message.ctx_;
-    void* dx = ctx->buf(1, buf.size() * CD);
+    const DevRange x = stage_in(*ctx, 1, buf.data(), buf.size() * CD);
     void* d16 = ctx->buf(3, buf.size() * sizeof(std::complex<int16_t>));
-    ctx->h2d(dx, buf.data(), buf.size() * CD);
-    check(ofdm_double_to_int16(ctx->ctx, (const double*)dx, buf.size(), (int16_t*)d16, nullptr), "ofdm_double_to_int16");
+    check(ofdm_double_to_int16(ctx->ctx, (const double*)x.d, buf.size(), (int16_t*)d16, ctx->stream()),
+          "ofdm_double_to_int16");
     ctx->d2h(int16_buf.data(), d16, buf.size() * sizeof(std::complex<int16_t>));
     return int16_buf;
 }
@@ -451,9 +483,10 @@ void FRAME_FORM::form_int16_to_double()
     COMPAT_TRACE("FRAME_FORM::form_int16_to_double");
     auto& ctx = message.ctx_;
     const size_t n = from_sdr_int16_buf.size();
-    void* d16 = ctx->buf(6, n * sizeof(std::complex<int16_t>));
-    void* dx = ctx->buf(5, n * CD);
-    ctx->h2d(d16, from_sdr_int16_buf.data(), n * sizeof(std::complex<int16_t>));
-    check(ofdm_int16_to_double(ctx->ctx, (const int16_t*)d16, n, (double*)dx, nullptr), "ofdm_int16_to_double");
-    ctx->d2h(from_sdr_buf.data(), dx, n * CD);
+    const DevRange in = stage_in(*ctx, 6, from_sdr_int16_buf.data(), n * sizeof(std::complex<int16_t>));
+    const DevRange out = stage_out_only(*ctx, 5, from_sdr_buf.data(), std::min(n, from_sdr_buf.size()) * CD);
+    check(ofdm_int16_to_double(ctx->ctx, (const int16_t*)in.d, std::min(n, from_sdr_buf.size()), (double*)out.d,
+                               ctx->stream()),
+          "ofdm_int16_to_double");
+    stage_back(*ctx, out);
 }

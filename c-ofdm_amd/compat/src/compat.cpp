@@ -5,6 +5,7 @@
 #include <signal.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cctype>
 #include <cstdlib>
 #include <cstring>
@@ -78,6 +79,9 @@ Context::Context(const ofdm_params& p) : params(p)
 {
     check(ofdm_create(&params, device_index(), &ctx), "ofdm_create");
     check(ofdm_get_geometry(ctx, &geo), "ofdm_get_geometry");
+    ofdm_preamble.resize((size_t)geo.preamble_len);
+    check(ofdm_get_preamble(ctx, nullptr, reinterpret_cast<double*>(ofdm_preamble.data()), nullptr, nullptr),
+          "ofdm_get_preamble");
 }
 
 Context::~Context()
@@ -100,18 +104,166 @@ void* Context::buf(int slot, size_t bytes)
     return s.first;
 }
 
-void Context::h2d(void* dev, const void* host, size_t bytes)
+// ---------------------------------------------------------------- engine
+Engine& Context::engine()
 {
-    if (bytes) check(ofdm_memcpy_h2d(ctx, dev, host, bytes, nullptr), "ofdm_memcpy_h2d");
+    // one per thread, never destroyed: global FRAME_FORMs (rx.cpp) outlive
+    // the thread-local storage at exit, and a leaked stream is harmless
+    thread_local Engine* e = nullptr;
+    if (!e) {
+        auto* n = new Engine;
+        ofdm_params p = params_default();
+        check(ofdm_create(&p, device_index(), &n->ctx), "ofdm_create (compat engine)");
+        check(ofdm_stream_create(n->ctx, &n->stream), "ofdm_stream_create");
+        e = n;
+    }
+    return *e;
 }
 
-void Context::d2h(void* host, const void* dev, size_t bytes)
+void* Engine::stage(size_t bytes)
 {
-    if (bytes) check(ofdm_memcpy_d2h(ctx, host, dev, bytes, nullptr), "ofdm_memcpy_d2h");
+    const size_t need = (bytes + 255) & ~(size_t)255;
+    if (arena_used + need > arena_bytes) {
+        sync();  // every staged copy has landed: the arena is free
+        if (need > arena_bytes) {
+            if (arena) check(ofdm_host_free(ctx, arena), "ofdm_host_free");
+            arena = nullptr;
+            arena_bytes = 0;
+            const size_t nb = std::max<size_t>(need, (size_t)4 << 20);
+            void* h = nullptr;
+            check(ofdm_host_alloc(ctx, nb, &h), "ofdm_host_alloc");
+            arena = static_cast<char*>(h);
+            arena_bytes = nb;
+        }
+    }
+    void* p = arena + arena_used;
+    arena_used += need;
+    return p;
+}
+
+void Engine::h2d(void* dev, const void* host, size_t bytes)
+{
+    if (!bytes) return;
+    void* st = stage(bytes);
+    std::memcpy(st, host, bytes);
+    h2d_pinned(dev, st, bytes);
+}
+
+void Engine::h2d_pinned(void* dev, const void* pinned, size_t bytes)
+{
+    if (bytes) check(ofdm_memcpy_h2d(ctx, dev, pinned, bytes, stream), "ofdm_memcpy_h2d");
+}
+
+void Engine::d2h_pinned(void* pinned, const void* dev, size_t bytes)
+{
+    if (bytes) check(ofdm_memcpy_d2h(ctx, pinned, dev, bytes, stream), "ofdm_memcpy_d2h");
+}
+
+void Engine::d2h(void* host, const void* dev, size_t bytes)
+{
+    if (!bytes) {
+        sync();
+        return;
+    }
+    void* st = stage(bytes);
+    d2h_pinned(st, dev, bytes);
     sync();
+    std::memcpy(host, st, bytes);
 }
 
-void Context::sync() { check(ofdm_stream_synchronize(ctx, nullptr), "ofdm_stream_synchronize"); }
+void Engine::sync()
+{
+    check(ofdm_stream_synchronize(ctx, stream), "ofdm_stream_synchronize");
+    arena_used = 0;
+}
+
+// ---------------------------------------------------------------- mirrors
+namespace {
+std::mutex g_mirror_mu;
+std::vector<Mirror*> g_mirrors;
+
+// First and last differing 256-byte blocks of a and b over n bytes
+// ([lo, hi) in bytes); lo == hi when equal.
+void diff_span(const char* a, const char* b, size_t n, size_t& lo, size_t& hi)
+{
+    constexpr size_t B = 256;
+    size_t i = 0;
+    while (i < n && std::memcmp(a + i, b + i, std::min(B, n - i)) == 0) i += B;
+    if (i >= n) {
+        lo = hi = n;
+        return;
+    }
+    size_t j = n;
+    while (j > i) {
+        const size_t s = j > i + B ? ((j - 1) / B) * B : i;
+        const size_t st = std::max(s, i);
+        if (std::memcmp(a + st, b + st, j - st) != 0) break;
+        j = st;
+    }
+    lo = i;
+    hi = j;
+}
+}  // namespace
+
+Mirror::Mirror(std::shared_ptr<Context> c, void* h, size_t n) : ctx(std::move(c)), host(static_cast<char*>(h)), bytes(n)
+{
+    void* d = nullptr;
+    void* s = nullptr;
+    check(ofdm_device_alloc(ctx->ctx, std::max<size_t>(n, 1), &d), "ofdm_device_alloc");
+    dev = static_cast<char*>(d);
+    check(ofdm_host_alloc(ctx->ctx, std::max<size_t>(n, 1), &s), "ofdm_host_alloc");
+    shadow = static_cast<char*>(s);
+    std::memcpy(shadow, host, n);
+    Engine& e = ctx->engine();
+    e.h2d_pinned(dev, shadow, n);
+    e.sync();
+    std::lock_guard<std::mutex> lock(g_mirror_mu);
+    g_mirrors.push_back(this);
+}
+
+Mirror::~Mirror()
+{
+    {
+        std::lock_guard<std::mutex> lock(g_mirror_mu);
+        g_mirrors.erase(std::remove(g_mirrors.begin(), g_mirrors.end(), this), g_mirrors.end());
+    }
+    ofdm_device_free(ctx->ctx, dev);
+    ofdm_host_free(ctx->ctx, shadow);
+}
+
+void Mirror::push(const void* p, size_t n)
+{
+    const size_t off = static_cast<const char*>(p) - host;
+    size_t lo, hi;
+    diff_span(host + off, shadow + off, n, lo, hi);
+    if (lo == hi) return;  // the device already holds these bytes
+    std::memcpy(shadow + off + lo, host + off + lo, hi - lo);
+    ctx->engine().h2d_pinned(dev + off + lo, shadow + off + lo, hi - lo);
+}
+
+void Mirror::pull(const void* p, size_t n)
+{
+    const size_t off = static_cast<const char*>(p) - host;
+    Engine& e = ctx->engine();
+    e.d2h_pinned(shadow + off, dev + off, n);
+    e.sync();
+    std::memcpy(host + off, shadow + off, n);
+}
+
+Mirror* find_mirror(const void* p, size_t n)
+{
+    std::lock_guard<std::mutex> lock(g_mirror_mu);
+    for (Mirror* m : g_mirrors)
+        if (m->covers(p, n)) return m;
+    return nullptr;
+}
+
+FrameMirrors::~FrameMirrors() = default;
+
+void FrameMirrors::add(std::shared_ptr<Context> c, void* host, size_t bytes)
+{
+    m.push_back(std::make_unique<Mirror>(std::move(c), host, bytes));
+}
 
 std::shared_ptr<Context> context_for(const ofdm_params& p)
 {
@@ -196,7 +348,7 @@ complex_vector Modulation::mod(std::vector<uint8_t>& in)
     void* din = ctx_->buf(0, in.size());
     void* dout = ctx_->buf(1, n * sizeof(complex_double));
     ctx_->h2d(din, in.data(), in.size());
-    check(ofdm_map(ctx_->ctx, (const uint8_t*)din, in.size(), (double*)dout, nullptr), "ofdm_map");
+    check(ofdm_map(ctx_->ctx, (const uint8_t*)din, in.size(), (double*)dout, ctx_->stream()), "ofdm_map");
     ctx_->d2h(out.data(), dout, n * sizeof(complex_double));
     return out;
 }
@@ -209,7 +361,7 @@ std::vector<uint8_t> Modulation::demod(complex_vector& in)
     void* dp = ctx_->buf(0, n * sizeof(complex_double));
     void* db = ctx_->buf(1, nb);
     ctx_->h2d(dp, in.data(), n * sizeof(complex_double));
-    check(ofdm_demap(ctx_->ctx, (double*)dp, n, (uint8_t*)db, nullptr), "ofdm_demap");
+    check(ofdm_demap(ctx_->ctx, (double*)dp, n, (uint8_t*)db, ctx_->stream()), "ofdm_demap");
     ctx_->d2h(out.data(), db, nb);
     ctx_->d2h(in.data(), dp, n * sizeof(complex_double));  // clamped in place (modulation.cpp:70-75)
     return out;
@@ -224,7 +376,7 @@ std::vector<uint8_t> Modulation::bit_stream_converter(size_t ob, size_t ib, std:
     void* dout = ctx_->buf(1, n);
     ctx_->h2d(din, in.data(), in.size());
     size_t m = 0;
-    check(ofdm_bit_convert(ctx_->ctx, (const uint8_t*)din, in.size(), (int)ib, (int)ob, (uint8_t*)dout, &m, nullptr),
+    check(ofdm_bit_convert(ctx_->ctx, (const uint8_t*)din, in.size(), (int)ib, (int)ob, (uint8_t*)dout, &m, ctx_->stream()),
           "ofdm_bit_convert");
     ctx_->d2h(out.data(), dout, n);
     return out;

@@ -718,6 +718,35 @@ int ofdm_stream_synchronize(ofdm_ctx* c, void* st)
     return OFDM_OK;
 }
 
+int ofdm_host_alloc(ofdm_ctx* c, size_t bytes, void** h)
+{
+    if (!c || !h) return fail(OFDM_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipHostMalloc(h, std::max<size_t>(bytes, 1), hipHostMallocDefault));
+    return OFDM_OK;
+}
+int ofdm_host_free(ofdm_ctx* c, void* h)
+{
+    if (!c) return fail(OFDM_ERR_INVALID, "null ctx");
+    if (h) HIP_TRY(hipHostFree(h));
+    return OFDM_OK;
+}
+int ofdm_stream_create(ofdm_ctx* c, void** st)
+{
+    if (!c || !st) return fail(OFDM_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = nullptr;
+    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *st = s;
+    return OFDM_OK;
+}
+int ofdm_stream_destroy(ofdm_ctx* c, void* st)
+{
+    if (!c) return fail(OFDM_ERR_INVALID, "null ctx");
+    if (st) HIP_TRY(hipStreamDestroy((hipStream_t)st));
+    return OFDM_OK;
+}
+
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // Device scratch that only grows (contents not preserved).

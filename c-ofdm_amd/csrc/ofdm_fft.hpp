@@ -154,14 +154,17 @@ __device__ __forceinline__ void tw_store(const TwPiece<LOGN>& p, double2* __rest
     lds_tw[p.dst] = p.w;
 }
 
-// W_N^j (forward sign) from the LDS table.
-template <int LOGN>
+// W_N^j (forward sign) from the LDS table, for 0 <= j < JMAX. When JMAX <= 64
+// (every base twiddle of a radix-R pass with N/R <= 64, e.g. all radix-8
+// passes of N <= 512) the HI factor is HI[0] = (1, -0), whose product leaves
+// LO bit for bit: it is skipped.
+template <int LOGN, int JMAX = (1 << LOGN)>
 __device__ __forceinline__ double2 tw_get(const double2* __restrict__ lds_tw, int j)
 {
     constexpr int NHI = TwLds<LOGN>::NHI;
     const int lo = j & 63;
     const double2 wlo = lds_tw[NHI + (lo ^ ((lo >> 4) & 3))];
-    if constexpr (NHI == 1) return wlo;
+    if constexpr (NHI == 1 || JMAX <= 64) return wlo;
     return cmul(lds_tw[j >> 6], wlo);
 }
 
@@ -236,7 +239,7 @@ __device__ __forceinline__ PassTw<LOGN, R, NS, SIGN> pass_twiddles(int t, const 
     for (int u = 0; u < B; ++u) {
         if constexpr (NS > 1) {
             const int k = (t + T * u) & (NS - 1);
-            double2 w1 = tw_get<LOGN>(lds_tw, k * (N / (NS * R)));
+            double2 w1 = tw_get<LOGN, N / R>(lds_tw, k * (N / (NS * R)));
             if (SIGN > 0) w1.y = -w1.y;
             tw.w[u] = w1;
         }

@@ -77,7 +77,7 @@ __device__ __forceinline__ void stockham_pass32(float2 (&v)[8], int t, const dou
         const int k = b & (NS - 1);
         if constexpr (NS > 1) {
             // the base twiddle from the FP64 table (TwLds), rounded once
-            const double2 w64 = tw_get<LOGN>(lds_tw, k * (N / (NS * R)));
+            const double2 w64 = tw_get<LOGN, N / R>(lds_tw, k * (N / (NS * R)));
             float2 w1 = make_float2((float)w64.x, (float)w64.y);
             if (SIGN > 0) w1.y = -w1.y;
             float2 w = w1;
@@ -211,7 +211,7 @@ __device__ __forceinline__ void stockham_pass32x2(float4 (&v)[8], int t, const d
         const int b = t + T * u;
         const int k = b & (NS - 1);
         if constexpr (NS > 1) {
-            const double2 w64 = tw_get<LOGN>(lds_tw, k * (N / (NS * R)));
+            const double2 w64 = tw_get<LOGN, N / R>(lds_tw, k * (N / (NS * R)));
             float2 w1 = make_float2((float)w64.x, (float)w64.y);
             if (SIGN > 0) w1.y = -w1.y;
             float2 w = w1;

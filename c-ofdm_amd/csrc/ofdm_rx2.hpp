@@ -117,13 +117,12 @@ __device__ __forceinline__ void rx2_frame(const RxArgs& a, long f, const Rx2Lds&
         }
     }
     __syncthreads();  // both waves' pilots visible; the images are free
-    double2 chv[2];
-    if (chan_g) {
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {  // D <= 256 = 2 x 128
-            const int d = tid + 128 * u;
-            chv[u] = chan_g[d < D ? d : 0];
-        }
+    // two named registers, not an array (an array held across the barriers
+    // below went to scratch)
+    double2 chv0 = make_double2(0.0, 0.0), chv1 = make_double2(0.0, 0.0);
+    if (chan_g) {  // D <= 256 = 2 x 128
+        chv0 = chan_g[tid < D ? tid : 0];
+        chv1 = chan_g[tid + 128 < D ? tid + 128 : 0];
     }
     // phys_pilot_ampl = sum |pilot| / (P*S*pilot_ampl)   (Frame.cpp:76-80),
     // summed by wave 0 in rx_kernel's lane order
@@ -148,9 +147,8 @@ __device__ __forceinline__ void rx2_frame(const RxArgs& a, long f, const Rx2Lds&
         L.gain[i] = make_double2(coef.x * r / phys, -coef.y * r / phys);
     }
     if (chan_g) {
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-            if (tid + 128 * u < D) L.chl[tid + 128 * u] = chv[u];
+        if (tid < D) L.chl[tid] = chv0;
+        if (tid + 128 < D) L.chl[tid + 128] = chv1;
     }
     __syncthreads();
     auto emit = [&](int s, const double2 (&yw)[RX_DPT]) {

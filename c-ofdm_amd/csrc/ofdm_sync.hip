@@ -22,6 +22,7 @@
 // threshold decisions are bit-identical.
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <cfloat>
 #include <climits>
 #include <cstdint>
 
@@ -1087,9 +1088,11 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
         __syncthreads();  // the five transforms visible
     }
     {
-        // X[k + M*r] = sum_q W_S^{q k} W_G^{q r} F_q[k]; amp stored fftshifted:
-        // shifted[i] = spec[(i + S/2) % S]  (Frame.hpp:300-305)
+        // X[k + M*r] = sum_q W_S^{q k} W_G^{q r} F_q[k]; stored fftshifted:
+        // shifted[i] = spec[(i + S/2) % S]  (Frame.hpp:300-305). The window
+        // argmax below works on |X|^2 and takes hypot only where it must.
         constexpr int half5 = S5 / 2;
+        double2* spec = img;
         double2 twg[G - 1];
 #pragma unroll
         for (int q = 1; q < G; ++q) twg[q - 1] = c.tw_full[(long)q * M];
@@ -1104,7 +1107,7 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
                 const double2 fq = img[q * M + lds_swz(k)];
                 tq[q] = q == 0 ? fq : cmul(fq, twk[q - 1]);
             }
-            __syncthreads();  // every transform read: amp overwrites them
+            __syncthreads();  // every transform read: the spectrum overwrites them
 #pragma unroll
             for (int r = 0; r < G; ++r) {
                 double2 acc = tq[0];
@@ -1112,13 +1115,20 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
                 for (int q = 1; q < G; ++q)
                     acc = cadd(acc, cmul(tq[q], (q * r) % G ? twg[(q * r) % G - 1] : make_double2(1.0, 0.0)));
                 const int idx = k + M * r;
-                amp[(idx + half5) % S5] = hypot(acc.x, acc.y);
+                spec[(idx + half5) % S5] = acc;
             }
         }
-        __syncthreads();  // amp visible
-        // first argmax inside each pilot window [borders[i], borders[i+1]), i != P/2
-        // (std::max_element: 8-lane groups, the larger value, the lower index on ties)
+        __syncthreads();  // spectrum visible
+        // first argmax of |X| = hypot inside each pilot window [borders[i],
+        // borders[i+1]), i != P/2 (std::max_element: 8-lane groups, the larger
+        // value, the lower index on ties). Decided on e = |X|^2 (two products,
+        // one sum: relative error <= 2u, u = 2^-53) where the runner-up e2 <
+        // e1 * (1 - 64u): then every other element's hypot (error <= 4u) is
+        // strictly below the winner's, so the winner is hypot's first maximum.
+        // Otherwise (near-ties, or a non-finite element) the group takes
+        // hypot of its window, as cfo_kernel does.
         constexpr int AG = 8;
+        constexpr double SURE = 1.0 - 64.0 * 0x1.0p-53;
         for (int i0 = 0; i0 <= c.P; i0 += 128 / AG) {
             const int i = i0 + tid / AG, l = tid % AG;
             const bool act = i <= c.P;
@@ -1127,23 +1137,56 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
                 lo = c.borders[i];
                 hi = c.borders[i + 1];
             }
-            double bv = -1.0;
-            int bi = INT_MAX;
-            for (int j = lo + l; j < hi; j += AG)
-                if (bv < amp[j]) {
-                    bv = amp[j];
+            double bv = -1.0, sv = -1.0;  // best and runner-up |X|^2 (below every magnitude)
+            int bi = INT_MAX, odd = 0;
+            for (int j = lo + l; j < hi; j += AG) {
+                const double2 z = spec[j];
+                const double e = add_rn(mul_rn(z.x, z.x), mul_rn(z.y, z.y));
+                odd |= !(e <= DBL_MAX);  // NaN or inf: hypot decides
+                if (bv < e) {
+                    sv = bv;
+                    bv = e;
                     bi = j;
-                }
-#pragma unroll
-            for (int o = 1; o < AG; o <<= 1) {
-                const double ov = __shfl_xor(bv, o);
-                const int oi = __shfl_xor(bi, o);
-                if (ov > bv || (ov == bv && oi < bi)) {
-                    bv = ov;
-                    bi = oi;
+                } else if (sv < e) {
+                    sv = e;
                 }
             }
-            if (act && l == 0) wsum[i] = lo < hi ? (isnan(amp[lo]) ? lo : bi) : hi;
+#pragma unroll
+            for (int o = 1; o < AG; o <<= 1) {
+                const double ov = __shfl_xor(bv, o), os = __shfl_xor(sv, o);
+                const int oi = __shfl_xor(bi, o);
+                odd |= __shfl_xor(odd, o);
+                if (ov > bv || (ov == bv && oi < bi)) {
+                    sv = fmax(bv, fmax(sv, os));
+                    bv = ov;
+                    bi = oi;
+                } else {
+                    sv = fmax(sv, fmax(ov, os));
+                }
+            }
+            bool first_nan = false;
+            if (odd || !(sv < bv * SURE)) {  // uniform within the 8-lane group
+                bv = -1.0;
+                bi = INT_MAX;
+                for (int j = lo + l; j < hi; j += AG) {
+                    const double h = hypot(spec[j].x, spec[j].y);
+                    if (bv < h) {
+                        bv = h;
+                        bi = j;
+                    }
+                }
+#pragma unroll
+                for (int o = 1; o < AG; o <<= 1) {
+                    const double ov = __shfl_xor(bv, o);
+                    const int oi = __shfl_xor(bi, o);
+                    if (ov > bv || (ov == bv && oi < bi)) {
+                        bv = ov;
+                        bi = oi;
+                    }
+                }
+                first_nan = lo < hi && isnan(hypot(spec[lo].x, spec[lo].y));
+            }
+            if (act && l == 0) wsum[i] = lo < hi ? (first_nan ? lo : bi) : hi;
         }
         __syncthreads();  // window maxima visible
         if (tid == 0) {
@@ -1250,6 +1293,12 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
         for (int i = t; i < a.P; i += T) acc += hypot(pil[i].x, pil[i].y);
         acc = block_sum2<T>(make_double2(acc, 0.0), red).x;
         const double phys = acc / ((double)a.P * a.pilot_ampl);
+        // arg((F/phys)/coef/mod_pre) (Frame.hpp:397-405 over FFT_FORM::read,
+        // Frame.cpp:82-93): only the angle is used, so the two complex
+        // divisions become products with the conjugates (same argument: a
+        // positive real factor |coef|^2 |mod_pre|^2 phys apart), for a finite
+        // positive phys; otherwise the reference's divisions verbatim
+        const bool plain = phys > 0.0 && phys <= DBL_MAX;  // uniform
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int i = t + T * u;
@@ -1257,8 +1306,14 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
                 const int j = dslot[u];
                 const double2 p0 = make_double2(pil[j].x / phys, pil[j].y / phys);
                 const double2 coef = cdiv_exact(p0, p0);
-                const double2 fs = make_double2(dat[i].x / phys, dat[i].y / phys);
-                const double2 q = cdiv_exact(cdiv_exact(fs, coef), mpre[u]);
+                double2 q;
+                if (plain) {
+                    q = cmul_exact(cmul_exact(dat[i], make_double2(coef.x, -coef.y)),
+                                   make_double2(mpre[u].x, -mpre[u].y));
+                } else {
+                    const double2 fs = make_double2(dat[i].x / phys, dat[i].y / phys);
+                    q = cdiv_exact(cdiv_exact(fs, coef), mpre[u]);
+                }
                 ph[i] = atan2(q.y, q.x);
             }
         }
@@ -1334,11 +1389,10 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
             th = add_rn(add_rn(mul_rn(-b, (double)a.D) / 2, mul_rn((double)(i - half), b)), aa);
         double sn, cs;
         sincos(th, &sn, &cs);
-        // the reciprocal of the unit phasor as conj / |.|^2 (one division; within
-        // 2 ulp of the exactly rounded quotient, which rx's multiply does not
-        // reproduce anyway: the reference divides each point)
-        const double r = 1.0 / (cs * cs + sn * sn);
-        chan[i] = a.chan_recip ? make_double2(cs * r, -sn * r) : make_double2(cs, sn);
+        // the reciprocal of the unit phasor as its conjugate (|h|^2 = 1 within
+        // 2u: the product differs from the reference's per-point division by
+        // a few ulps, as the multiply by a reciprocal does anyway)
+        chan[i] = a.chan_recip ? make_double2(cs, -sn) : make_double2(cs, sn);
     }
     __syncthreads();  // psi visible
     // message symbols: theta(m) = A_s + B_s m over the CP-stripped body

@@ -111,6 +111,10 @@ SIGNATURES = {
     "ofdm_rx_stream_shard": (_I, [_V, _V, _V, _SZ, _L, _L, _L, _SZ, _L, _V, _V, _V, _V, C.POINTER(_SZ), _V, _SZ,
                                   C.POINTER(_SZ), C.POINTER(_L), _V]),
     "ofdm_stream_shard_margins": (_I, [_V, C.POINTER(_L), C.POINTER(_L)]),
+    "ofdm_host_alloc": (_I, [_V, _SZ, C.POINTER(_V)]),
+    "ofdm_host_free": (_I, [_V, _V]),
+    "ofdm_stream_create": (_I, [_V, C.POINTER(_V)]),
+    "ofdm_stream_destroy": (_I, [_V, _V]),
     "ofdm_walk_tuning_default": (_I, [C.POINTER(WalkTuning)]),
     "ofdm_get_walk_tuning": (_I, [_V, C.POINTER(WalkTuning)]),
     "ofdm_set_walk_tuning": (_I, [_V, C.POINTER(WalkTuning)]),
@@ -130,7 +134,10 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise OSError(f"{LIB_PATH} missing: run `make -C c-ofdm_amd` (no CPU fallback exists)")
         L = C.CDLL(LIB_PATH)
+        variant = "OFDM_MI355X_LIB" in os.environ  # an A/B build of an older tree may lack newer entries
         for name, (res, args) in SIGNATURES.items():
+            if variant and not hasattr(L, name):
+                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -133,6 +133,12 @@ int ofdm_memcpy_h2d(ofdm_ctx* ctx, void* dst, const void* src, size_t bytes, voi
 int ofdm_memcpy_d2h(ofdm_ctx* ctx, void* dst, const void* src, size_t bytes, void* stream);
 int ofdm_memset_device(ofdm_ctx* ctx, void* dst, int value, size_t bytes, void* stream);
 int ofdm_stream_synchronize(ofdm_ctx* ctx, void* stream);
+/* Page-locked host memory (DMA-able: copies from / to it are asynchronous). */
+int ofdm_host_alloc(ofdm_ctx* ctx, size_t bytes, void** hptr);
+int ofdm_host_free(ofdm_ctx* ctx, void* hptr);
+/* A non-blocking HIP stream on the ctx's device, and its destruction. */
+int ofdm_stream_create(ofdm_ctx* ctx, void** stream);
+int ofdm_stream_destroy(ofdm_ctx* ctx, void* stream);
 
 /* ---- tx: FRAME_FORM::write (Frame.cpp:235-237) -> OFDM_FORM::write
  *      (Frame.cpp:185-198) -> Modulation::mod (modulation.cpp:39-50) +

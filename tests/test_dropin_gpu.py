@@ -171,3 +171,62 @@ def test_reference_main_writes_python_code_file_contract(tmp_path):
     _, ocons, obytes = O.decode_frame(G, x[pb: pb + g["preamble_len"] + g["message_len"]])
     assert np.abs(cons - ocons).max() / np.abs(ocons).max() < 1e-9
     assert obytes.tobytes() == GD["payload"].tobytes()
+
+
+SELFTEST = os.path.join(ROOT, "c-ofdm_amd", "bin", "compat_selftest")
+
+
+def gapped_capture(txf, frame_len):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from dropin_rx_timing import gapped_capture as gc
+    gc(txf, frame_len)
+
+
+@pytest.mark.parametrize("name", ["D", "G"])
+def test_compat_device_mirrors_equal_staged_path(tmp_path, name):
+    """c-ofdm_amd/apps/compat_selftest: a FRAME_FORM's device-mirrored buffers
+    (the forms move only what the host changed, copy back what they change in
+    place) give bit-identical results to the same members on a plain vector
+    (staged through the pinned arena): fresh frames, the same frame copied in
+    again after the in-place members, partial host writes between members,
+    the int16 ring and direct host writes to from_sdr_buf; and
+    PREAMBLE_FORM::chan_char equals Frame.hpp:375-385 on fft()'s output."""
+    cfg = write_config(tmp_path, {"D": D, "G": G}[name])
+    r = run([SELFTEST, cfg, "12"], tmp_path)
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+    assert "SELFTEST OK" in r.stdout
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(REF_BIN, "rx")), reason="drop-in reference apps not built")
+def test_reference_tx_rx_apps_stream_120_frames(tmp_path):
+    """The reference's own tx.cpp frames a 120-frame payload file into the SDR
+    stand-in's int16 capture (data/tx.bin layout); its own rx.cpp streams the
+    capture (with 0-3000-sample silences between the bursts) through the ring
+    buffer, the detection walk and the per-frame sync chain on the
+    device-mirrored FRAME_FORM, and writes every payload it decodes to
+    Res.wav. Every written payload equals a sent one, in order, and rx.cpp's
+    walk locates at least 90% of the frames (its T2 search tests blocks on a
+    256-sample grid, Frame.hpp:164, so a frame whose marker straddles two grid
+    blocks can be missed, as in the reference)."""
+    nfr = 120
+    write_config(tmp_path, D, iterations=nfr + 60)
+    g = O.geometry(D)
+    pay = g["bytes_per_frame"] - 8
+    body = bytes((i * 131 + 7 + (i // pay) * 17) & 0xFF for i in range(nfr * pay))
+    (tmp_path / "FlyMeToTheMoon_mono.wav").write_bytes(body)
+    txf = tmp_path / "tx.bin"
+    r = run([os.path.join(REF_BIN, "tx")], tmp_path, {"OFDM_SDR_TX_FILE": str(txf)})
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert np.fromfile(txf, np.int16).size == 2 * nfr * g["frame_len"]
+    gapped_capture(txf, g["frame_len"])  # silences between the bursts, as on air
+    r = run([os.path.join(REF_BIN, "rx")], tmp_path, {"OFDM_SDR_RX_FILE": str(txf)}, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = (tmp_path / "Res.wav").read_bytes()
+    chunks = [body[i * pay:(i + 1) * pay] for i in range(nfr)]
+    got = [res[i * pay:(i + 1) * pay] for i in range(len(res) // pay)]
+    assert len(res) % pay == 0
+    idx = [chunks.index(c) if c in chunks else -1 for c in got]
+    assert -1 not in idx, f"{idx.count(-1)} of {len(got)} written payloads match no sent frame"
+    assert idx == sorted(idx) and len(set(idx)) == len(idx)
+    assert len(got) >= 0.9 * nfr, f"only {len(got)} of {nfr} frames decoded"

@@ -27,17 +27,38 @@ sys.path[:0] = [os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle"), os.pa
 REF_BIN = os.path.join(ROOT, "oracle", "_ref")
 
 
+STAGES = ("T2SIN", "PILOT_SINH", "FREQ_PHASE_SINH", "PFC", "MAC")
+
+
 def parse_log(text):
-    frames, refills = [], []
+    frames, refills, stages = [], [], {k: [] for k in STAGES}
     for line in text.splitlines():
         kv = dict(re.findall(r"(\w+):(\S+)", line))
         if "TIME" not in kv:
             continue
         if "SEQ" in kv and "SDR" not in kv:
             frames.append(float(kv["TIME"]))
+            for k in STAGES:
+                if k in kv:
+                    stages[k].append(float(kv[k]))
         elif "SDR" in kv:
             refills.append(float(kv.get("CONVERT", "nan")))
-    return frames, refills
+    return frames, refills, stages
+
+
+def gapped_capture(txf, frame_len, seed=4, gap_max=3000):
+    """The tx app's back-to-back frames with random 0..gap_max-sample silences
+    between them (the air between bursts, as the config-4 stream has): rx.cpp
+    tests T2 blocks on a 256-sample grid from the end of the previous frame's
+    message, so back-to-back frames put every other marker across two blocks."""
+    import numpy as np
+    iq = np.fromfile(txf, np.int16).reshape(-1, frame_len, 2)
+    rng = np.random.default_rng(seed)
+    parts = []
+    for f in iq:
+        parts += [np.zeros((int(rng.integers(0, gap_max + 1)), 2), np.int16), f]
+    parts.append(np.zeros((frame_len, 2), np.int16))
+    np.concatenate(parts).tofile(txf)
 
 
 def main():
@@ -56,15 +77,16 @@ def main():
         env = dict(os.environ, OFDM_SDR_TX_FILE=txf)
         r = subprocess.run([os.path.join(REF_BIN, "tx")], cwd=d, env=env, capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
+        gapped_capture(txf, g["frame_len"])
         env = dict(os.environ, OFDM_SDR_RX_FILE=txf)
         r = subprocess.run([os.path.join(REF_BIN, "rx")], cwd=d, env=env, capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
         with open(os.path.join(d, "LOG.txt")) as f:
-            ours, refills = parse_log(f.read())
+            ours, refills, stages = parse_log(f.read())
         with open(os.path.join(d, "Res.wav"), "rb") as f:
             res = f.read()
     chunks = {body[i * pay:(i + 1) * pay] for i in range(args.frames)}
-    out = {"what": "rx.cpp per-frame iteration time (LOG.txt TIME of iterations that decoded a frame without a "
+    out = {"frames_sent": args.frames, "what": "rx.cpp per-frame iteration time (LOG.txt TIME of iterations that decoded a frame without a "
                    "ring refill), reference rx.cpp compiled unchanged on the drop-in layer",
            "config": "D (config/config.txt)", "frames_decoded": len(ours),
            "frames_written": len(res) // pay,
@@ -73,9 +95,12 @@ def main():
            "p10_us": sorted(ours)[len(ours) // 10] * 1e6 if ours else None,
            "p90_us": sorted(ours)[9 * len(ours) // 10] * 1e6 if ours else None,
            "refill_convert_median_us": statistics.median(refills) * 1e6 if refills else None,
+           "stage_median_us": {k: statistics.median(v) * 1e6 for k, v in stages.items() if v},
            # parse_log over the reference's committed LOG.txt (9 430 frame iterations; its
            # authors' machine, FFTW on the CPU), evaluated in the build container
            "reference_LOG_txt_median_us": 238.42,
+           "reference_LOG_txt_stage_median_us": {"T2SIN": 17.2, "PILOT_SINH": 57.2, "FREQ_PHASE_SINH": 84.2, "PFC": 27.2,
+                                                 "MAC": 3.3},
            "reference_note": "the reference's committed LOG.txt (its authors' machine, FFTW, CPU)"}
     print(json.dumps(out), flush=True)
 
