@@ -6,7 +6,9 @@
 //      plain vector (staged through the arena, no mirror) — for fresh
 //      frames, for the same frame copied in again after the in-place
 //      members ran (the host bytes then equal neither the shadow's nor the
-//      device's), and for partial host writes between members;
+//      device's), for partial host writes between members, and with the
+//      run-ahead chain (ofdm_compat::Chain) served, refused (another CFO
+//      value, a skipped member) and taken in another order;
 //   2. form_int16_to_double, find_t2sin, find_preamble and corr on the
 //      mirrored rx ring equal the staged path, also after direct host writes
 //      to from_sdr_buf;
@@ -102,6 +104,44 @@ int main(int argc, char** argv)
             std::copy(f.begin(), f.end(), rx.buf.begin());
             std::copy(f.begin(), f.end(), plain.begin());
             run_chain("recopied", k);
+        }
+        if (k % 4 == 3) {
+            // the run-ahead chain must not be served for another CFO value,
+            // nor out of order (fft before chan_char_lq, cp_freq_sinh skipped)
+            std::copy(f.begin(), f.end(), rx.buf.begin());
+            std::copy(f.begin(), f.end(), plain.begin());
+            double c1 = rx.preamble.pilot_freq_sinh(), c2 = pre2.pilot_freq_sinh();
+            CHECK(c1 == c2, "other-cfo frame %d: pilot_freq_sinh", k);
+            c1 += 1e-7;
+            c2 += 1e-7;
+            rx.message_with_preamble.freq_shift(c1);
+            mwp2.freq_shift(c2);
+            CHECK(same(rx.buf.data() + t2, plain.data() + t2, span), "other-cfo frame %d: freq_shift", k);
+            rx.message_with_preamble.pr_phase_sinh(rx.preamble.ofdm_preamble.data(), rx.preamble.size);
+            mwp2.pr_phase_sinh(pre2.ofdm_preamble.data(), pre2.size);
+            CHECK(same(rx.buf.data() + t2, plain.data() + t2, span), "other-cfo frame %d: pr_phase_sinh", k);
+            auto f1 = rx.message.fft(), f2 = msg2.fft();
+            CHECK(same(f1.data(), f2.data(), f1.size()), "other-cfo frame %d: fft", k);
+            auto& h1 = rx.preamble.chan_char_lq();
+            auto& h2 = pre2.chan_char_lq();
+            CHECK(same(h1.data(), h2.data(), h1.size()), "other-cfo frame %d: chan_char_lq", k);
+            // the full chain in the reference's order again, fft before chan_char_lq
+            std::copy(f.begin(), f.end(), rx.buf.begin());
+            std::copy(f.begin(), f.end(), plain.begin());
+            c1 = rx.preamble.pilot_freq_sinh();
+            c2 = pre2.pilot_freq_sinh();
+            rx.message_with_preamble.freq_shift(c1);
+            mwp2.freq_shift(c2);
+            rx.message_with_preamble.cp_freq_sinh();
+            mwp2.cp_freq_sinh();
+            rx.message_with_preamble.pr_phase_sinh(rx.preamble.ofdm_preamble.data(), rx.preamble.size);
+            mwp2.pr_phase_sinh(pre2.ofdm_preamble.data(), pre2.size);
+            auto g1 = rx.message.fft(), g2 = msg2.fft();
+            CHECK(same(g1.data(), g2.data(), g1.size()), "fft-first frame %d: fft", k);
+            auto& q1 = rx.preamble.chan_char_lq();
+            auto& q2 = pre2.chan_char_lq();
+            CHECK(same(q1.data(), q2.data(), q1.size()), "fft-first frame %d: chan_char_lq", k);
+            CHECK(same(rx.buf.data() + t2, plain.data() + t2, span), "fft-first frame %d: buffer", k);
         }
         if (k % 3 == 2) {
             // partial host writes between members

@@ -23,7 +23,10 @@ void check(int rc, const char* what);  // throws std::runtime_error(ofdm_last_er
 
 // Per-thread transfers: the stream every compat kernel of this thread runs
 // on, and a pinned arena for staging pageable host data (reset at each sync,
-// so a staged copy's source stays intact until its DMA is done).
+// so a staged copy's source stays intact until its copy is done). Copies to
+// and from pinned memory are kernels on the same stream (ofdm_copy): the
+// per-frame transfers are small, and a DMA-engine hand-off between two
+// kernels costs more than the copy itself.
 struct Engine {
     ofdm_ctx* ctx = nullptr;  // the context that created the stream (kept alive)
     void* stream = nullptr;
@@ -55,6 +58,12 @@ struct Context {
 
 private:
     std::vector<std::pair<void*, size_t>> slots_;
+
+public:
+    const int* zero_index();  // a device int holding 0 (uploaded once)
+
+private:
+    int* zero_ = nullptr;
 };
 
 // Device mirror of one host buffer (FRAME_FORM::buf, from_sdr_buf,
@@ -73,6 +82,10 @@ struct Mirror {
     size_t bytes = 0;
     char* dev = nullptr;
     char* shadow = nullptr;
+    size_t gen = 0;  // bumped by every upload and every copy back (content changed)
+    // [stale_lo, stale_hi): bytes whose device copy runs ahead of the shadow
+    // (the run-ahead chain works in place); the next push or write settles it
+    size_t stale_lo = 0, stale_hi = 0;
     Mirror(std::shared_ptr<Context> c, void* host, size_t bytes);
     ~Mirror();
     Mirror(const Mirror&) = delete;
@@ -85,17 +98,60 @@ struct Mirror {
     void* device(const void* p) const { return dev + (static_cast<const char*>(p) - host); }
     void push(const void* p, size_t n);
     void pull(const void* p, size_t n);
+    void settle();  // device := shadow on the stale range
 };
 
 // The registered mirror covering [p, p + n), or nullptr.
 Mirror* find_mirror(const void* p, size_t n);
 
-// A FRAME_FORM's mirrors (registered while alive).
+// The reference apps' per-frame sync chain (main.cpp:60-71, rx.cpp:200-216)
+// run ahead on the device. When PREAMBLE_FORM::pilot_freq_sinh is called on a
+// FRAME_FORM's own preamble form, the whole chain is enqueued behind the CFO
+// kernel on copies of the frame's device image: freq_shift by that CFO,
+// cp_freq_sinh, pr_phase_sinh with the context preamble, chan_char_lq and
+// the message FFT, each state and result copied to pinned memory. The later
+// member calls are then served from those results, without a device round
+// trip, when (and only when) their inputs are the ones speculated: the call
+// order, the same CFO value (bitwise), the context's own preamble, and host
+// bytes of the frame region unchanged since the previous member returned.
+// Any other call runs the ordinary path and ends the speculation; served
+// results are the same kernels on the same inputs, so bit-identical.
+struct Chain {
+    const void* pre_form = nullptr;  // identities of the FRAME_FORM's forms
+    const void* msg_form = nullptr;
+    const void* mwp_form = nullptr;
+    char* region = nullptr;  // host message_with_preamble region (buf + T2sin_size)
+    size_t region_bytes = 0, pre_bytes = 0, chan_bytes = 0, cons_bytes = 0;
+    std::shared_ptr<Context> pre_ctx, msg_ctx, mwp_ctx;
+    int stage = 0;  // 1: freq_shift next, 2: cp_freq_sinh, 3: pr_phase_sinh, 4: chan_char_lq / fft
+    size_t gen = 0;  // the frame mirror's generation the stage was reached at
+    bool chan_served = false, fft_served = false;
+    double cfo = 0.0;
+    // the states after freq_shift / cp / phase (pinned), results, events
+    char* hstate[3] = {};
+    char *dchan = nullptr, *hchan = nullptr, *dcons = nullptr, *hcons = nullptr;
+    double *dcfo = nullptr, *hcfo = nullptr;
+    void* ev[6] = {};  // cfo, state 0..2, chan, cons
+    ~Chain();
+    bool alloc(Engine& e);
+};
+
+// A FRAME_FORM's mirrors and run-ahead chain (registered while alive).
 struct FrameMirrors {
     std::vector<std::unique_ptr<Mirror>> m;
+    Chain chain;
+    FrameMirrors();
     ~FrameMirrors();
     void add(std::shared_ptr<Context> c, void* host, size_t bytes);
 };
+
+// The chain of the FRAME_FORM owning `form` (one of its three OFDM forms), or nullptr.
+Chain* chain_of(const void* form);
+// True when the host bytes [p, p + n) of a mirrored range equal its shadow
+// and the mirror is still at generation `gen`.
+bool mirror_clean(const void* p, size_t n, size_t gen);
+// The generation of the mirror covering [p, p + n) (0 if none).
+size_t mirror_gen(const void* p, size_t n);
 
 std::shared_ptr<Context> context_for(const ofdm_params& p);
 ofdm_params params_from(ConfigMap& config);

@@ -12,7 +12,9 @@
 #include "OFDM/Frame.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
+#include <optional>
 #include <cstdlib>
 #include <cstring>
 
@@ -25,16 +27,26 @@ namespace {
 
 constexpr size_t CD = sizeof(complex_double);
 
-// OFDM_COMPAT_TRACE=1: one stderr line per compat call (diagnostics).
+// OFDM_COMPAT_TRACE=1: one stderr line per compat call with its wall time
+// in microseconds (diagnostics).
 bool trace_on()
 {
     static const bool on = std::getenv("OFDM_COMPAT_TRACE") != nullptr;
     return on;
 }
-#define COMPAT_TRACE(name)                                           \
-    do {                                                             \
-        if (trace_on()) std::fprintf(stderr, "[compat] %s\n", name); \
-    } while (0)
+struct TraceScope {
+    const char* name;
+    std::chrono::steady_clock::time_point t0;
+    explicit TraceScope(const char* n) : name(n), t0(std::chrono::steady_clock::now()) {}
+    ~TraceScope()
+    {
+        const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        std::fprintf(stderr, "[compat] %s %.1f\n", name, us);
+    }
+};
+#define COMPAT_TRACE(name) \
+    std::optional<TraceScope> trace_scope_; \
+    if (trace_on()) trace_scope_.emplace(name)
 
 ofdm_params form_params(ConfigMap& config, int num_symb, int mod)
 {
@@ -67,7 +79,10 @@ DevRange stage_in(Context& ctx, int slot, const void* h, size_t n)
 // A device range the kernel is about to overwrite entirely: no upload.
 DevRange stage_out_only(Context& ctx, int slot, void* h, size_t n)
 {
-    if (ofdm_compat::Mirror* m = ofdm_compat::find_mirror(h, n)) return {m->device(h), m, h, n};
+    if (ofdm_compat::Mirror* m = ofdm_compat::find_mirror(h, n)) {
+        m->settle();
+        return {m->device(h), m, h, n};
+    }
     return {ctx.buf(slot, std::max<size_t>(n, 1)), nullptr, h, n};
 }
 
@@ -78,6 +93,33 @@ void stage_back(Context& ctx, const DevRange& r)
         r.m->pull(r.h, r.n);
     else
         ctx.d2h(r.h, r.d, r.n);
+}
+
+// The run-ahead chain (ofdm_compat::Chain) of the FRAME_FORM that owns `form`,
+// when it is at `stage` and the frame region's host bytes [p, p + n) are the
+// ones it speculated on; otherwise the chain ends (nullptr).
+ofdm_compat::Chain* served(const void* form, int stage, const void* p, size_t n)
+{
+    ofdm_compat::Chain* ch = ofdm_compat::chain_of(form);
+    if (!ch) return nullptr;
+    if (ch->stage == stage && ofdm_compat::mirror_clean(p, n, ch->gen)) return ch;
+    ch->stage = 0;
+    return nullptr;
+}
+
+// Serve state k (after freq_shift / cp_freq_sinh / pr_phase_sinh) of the
+// chain: host region and shadow take it; the device image (which the chain
+// advanced in place to the last state) equals the shadow again at k = 2.
+void serve_state(Context& ctx, ofdm_compat::Chain& ch, int k)
+{
+    ofdm_compat::Engine& e = ctx.engine();
+    check(ofdm_event_synchronize(e.ctx, ch.ev[1 + k]), "ofdm_event_synchronize");
+    ofdm_compat::Mirror* m = ofdm_compat::find_mirror(ch.region, ch.region_bytes);
+    std::memcpy(ch.region, ch.hstate[k], ch.region_bytes);
+    const size_t off = ch.region - m->host;
+    std::memcpy(m->shadow + off, ch.hstate[k], ch.region_bytes);
+    if (k == 2 && m->stale_lo == off && m->stale_hi == off + ch.region_bytes) m->stale_lo = m->stale_hi = 0;
+    ch.stage = k + 2;
 }
 
 }  // namespace
@@ -284,6 +326,16 @@ complex_vector OFDM_FORM::fft()
 {
     COMPAT_TRACE("OFDM_FORM::fft");
     const size_t np = (size_t)usefull_size;
+    if (ofdm_compat::Chain* ch = served(this, 4, output[0], (size_t)size * CD)) {
+        if (this == ch->msg_form && !ch->fft_served && np * CD == ch->cons_bytes) {
+            check(ofdm_event_synchronize(ctx_->engine().ctx, ch->ev[5]), "ofdm_event_synchronize");
+            std::memcpy(fft_task.restored_buf.data(), ch->hcons, ch->cons_bytes);
+            ch->fft_served = true;
+            if (ch->chan_served) ch->stage = 0;
+            return fft_task.restored_buf;
+        }
+        ch->stage = 0;
+    }
     const DevRange x = stage_in(*ctx_, 1, output[0], (size_t)size * CD);
     void* dc = ctx_->buf(2, np * CD);
     check(ofdm_rx_demod(ctx_->ctx, (const double*)x.d, 1, (size_t)size, nullptr, 0, (double*)dc, nullptr, nullptr,
@@ -296,6 +348,10 @@ complex_vector OFDM_FORM::fft()
 void OFDM_FORM::cp_freq_sinh()
 {
     COMPAT_TRACE("OFDM_FORM::cp_freq_sinh");
+    if (ofdm_compat::Chain* ch = served(this, 2, output[0], (size_t)size * CD)) {
+        if (this == ch->mwp_form) return serve_state(*ctx_, *ch, 1);
+        ch->stage = 0;
+    }
     const DevRange x = stage_in(*ctx_, 1, output[0], (size_t)size * CD);
     check(ofdm_cp_sync(ctx_->ctx, (double*)x.d, 1, (size_t)size, num_symb, ctx_->stream()), "ofdm_cp_sync");
     stage_back(*ctx_, x);
@@ -304,6 +360,12 @@ void OFDM_FORM::cp_freq_sinh()
 void OFDM_FORM::pr_phase_sinh(complex_double* pr, int pr_size)
 {
     COMPAT_TRACE("OFDM_FORM::pr_phase_sinh");
+    if (ofdm_compat::Chain* ch = served(this, 3, output[0], (size_t)size * CD)) {
+        if (this == ch->mwp_form && (size_t)pr_size == ctx_->ofdm_preamble.size() &&
+            std::memcmp(pr, ctx_->ofdm_preamble.data(), (size_t)pr_size * CD) == 0)
+            return serve_state(*ctx_, *ch, 2);
+        ch->stage = 0;
+    }
     const DevRange x = stage_in(*ctx_, 1, output[0], (size_t)size * CD);
     // the caller's preamble copy (main.cpp:63 / rx.cpp:208 pass
     // preamble.ofdm_preamble): when it holds the context's own ofdm_preamble,
@@ -325,6 +387,55 @@ void OFDM_FORM::pr_phase_sinh(complex_double* pr, int pr_size)
 double OFDM_FORM::pilot_freq_sinh()
 {
     COMPAT_TRACE("OFDM_FORM::pilot_freq_sinh");
+    ofdm_compat::Chain* ch = ofdm_compat::chain_of(this);
+    if (ch) ch->stage = 0;
+    if (ch && this == ch->pre_form && output[0] == (complex_double*)ch->region &&
+        ofdm_compat::find_mirror(ch->region, ch->region_bytes) && ch->alloc(ctx_->engine())) {
+        // the frame's whole message_with_preamble region on the device, then
+        // pilot_freq_sinh and the rest of main.cpp:60-66 behind it on copies
+        ofdm_compat::Engine& e = ctx_->engine();
+        const DevRange r = stage_in(*ctx_, 1, ch->region, ch->region_bytes);
+        void* st = e.stream;
+        check(ofdm_cfo_estimate(ctx_->ctx, (const double*)r.d, 1, (size_t)size, num_symb, ch->dcfo, st),
+              "ofdm_cfo_estimate");
+        e.d2h_pinned(ch->hcfo, ch->dcfo, sizeof(double));
+        check(ofdm_event_record(e.ctx, ch->ev[0], st), "ofdm_event_record");
+        // the chain runs in place on the frame's device image: it is marked
+        // stale (ahead of the shadow) until its last state is served
+        const size_t nw = ch->region_bytes / CD;
+        ofdm_ctx* mw = ch->mwp_ctx->ctx;
+        const int nsym = (int)(nw / (size_t)ofdm_len);
+        char* dr = static_cast<char*>(r.d);
+        r.m->stale_lo = ch->region - r.m->host;
+        r.m->stale_hi = r.m->stale_lo + ch->region_bytes;
+        check(ofdm_freq_shift(mw, (double*)dr, 1, nw, nw, ch->dcfo, st), "ofdm_freq_shift");
+        e.d2h_pinned(ch->hstate[0], dr, ch->region_bytes);
+        check(ofdm_event_record(e.ctx, ch->ev[1], st), "ofdm_event_record");
+        check(ofdm_cp_sync(mw, (double*)dr, 1, nw, nsym, st), "ofdm_cp_sync");
+        e.d2h_pinned(ch->hstate[1], dr, ch->region_bytes);
+        check(ofdm_event_record(e.ctx, ch->ev[2], st), "ofdm_event_record");
+        check(ofdm_phase_sync(mw, (double*)dr, 1, nw, nw, nullptr, 0, st), "ofdm_phase_sync");
+        e.d2h_pinned(ch->hstate[2], dr, ch->region_bytes);
+        check(ofdm_event_record(e.ctx, ch->ev[3], st), "ofdm_event_record");
+        check(ofdm_chan_estimate(ch->pre_ctx->ctx, (const double*)dr, 1, ch->pre_bytes / CD, (double*)ch->dchan,
+                                 ch->chan_bytes / CD, st),
+              "ofdm_chan_estimate");
+        e.d2h_pinned(ch->hchan, ch->dchan, ch->chan_bytes);
+        check(ofdm_event_record(e.ctx, ch->ev[4], st), "ofdm_event_record");
+        const size_t nm = (ch->region_bytes - ch->pre_bytes) / CD;
+        check(ofdm_rx_demod(ch->msg_ctx->ctx, (const double*)(dr + ch->pre_bytes), 1, nm, nullptr, 0,
+                            (double*)ch->dcons, nullptr, nullptr, nullptr, st),
+              "ofdm_rx_demod");
+        e.d2h_pinned(ch->hcons, ch->dcons, ch->cons_bytes);
+        check(ofdm_event_record(e.ctx, ch->ev[5], st), "ofdm_event_record");
+        check(ofdm_event_synchronize(e.ctx, ch->ev[0]), "ofdm_event_synchronize");
+        const double shift = *ch->hcfo;
+        ch->cfo = shift;
+        ch->stage = 1;
+        ch->gen = ofdm_compat::mirror_gen(ch->region, ch->region_bytes);
+        ch->chan_served = ch->fft_served = false;
+        return shift;
+    }
     const DevRange x = stage_in(*ctx_, 1, output[0], (size_t)size * CD);
     void* dc = ctx_->buf(4, sizeof(double));
     check(ofdm_cfo_estimate(ctx_->ctx, (const double*)x.d, 1, (size_t)size, num_symb, (double*)dc, ctx_->stream()),
@@ -337,6 +448,11 @@ double OFDM_FORM::pilot_freq_sinh()
 void OFDM_FORM::freq_shift(double& shift)
 {
     COMPAT_TRACE("OFDM_FORM::freq_shift");
+    if (ofdm_compat::Chain* ch = served(this, 1, output[0], (size_t)size * CD)) {
+        if (this == ch->mwp_form && std::memcmp(&shift, &ch->cfo, sizeof(double)) == 0)
+            return serve_state(*ctx_, *ch, 0);
+        ch->stage = 0;
+    }
     const DevRange x = stage_in(*ctx_, 1, output[0], (size_t)size * CD);
     void* dc = ctx_->buf(4, sizeof(double));
     ctx_->h2d(dc, &shift, sizeof(double));
@@ -393,13 +509,11 @@ int PREAMBLE_FORM::find_preamble(complex_vector& input, int start)
     if (start < 0 || start >= n) return -10;
     const long win = std::min<long>(n - start, (long)cor.size() + pr_sin_len);
     const DevRange x = stage_in(*ctx_, 5, input.data() + start, (size_t)win * CD);
-    int* ds = (int*)ctx_->buf(7, 2 * sizeof(int));
-    const int zero = 0;
-    ctx_->h2d(ds, &zero, sizeof(int));
-    check(ofdm_find_preamble(ctx_->ctx, (const double*)x.d, (size_t)win, ds, 1, ds + 1, ctx_->stream()),
+    int* ds = (int*)ctx_->buf(7, sizeof(int));
+    check(ofdm_find_preamble(ctx_->ctx, (const double*)x.d, (size_t)win, ctx_->zero_index(), 1, ds, ctx_->stream()),
           "ofdm_find_preamble");
     int idx = -10;
-    ctx_->d2h(&idx, ds + 1, sizeof(int));
+    ctx_->d2h(&idx, ds, sizeof(int));
     return idx < 0 ? idx : idx + start;
 }
 
@@ -419,6 +533,16 @@ complex_vector PREAMBLE_FORM::chan_char()
 complex_vector& PREAMBLE_FORM::chan_char_lq()
 {
     COMPAT_TRACE("PREAMBLE_FORM::chan_char_lq");
+    if (ofdm_compat::Chain* ch = served(this, 4, output[0], (size_t)size * CD)) {
+        if (this == ch->pre_form && !ch->chan_served && chan_est.size() * CD == ch->chan_bytes) {
+            check(ofdm_event_synchronize(ctx_->engine().ctx, ch->ev[4]), "ofdm_event_synchronize");
+            std::memcpy(chan_est.data(), ch->hchan, ch->chan_bytes);
+            ch->chan_served = true;
+            if (ch->fft_served) ch->stage = 0;
+            return chan_est;
+        }
+        ch->stage = 0;
+    }
     const DevRange x = stage_in(*ctx_, 1, output[0], (size_t)size * CD);
     void* dc = ctx_->buf(2, chan_est.size() * CD);
     check(ofdm_chan_estimate(ctx_->ctx, (const double*)x.d, 1, (size_t)size, (double*)dc, chan_est.size(),
@@ -453,6 +577,18 @@ FRAME_FORM::FRAME_FORM(const std::string& CONFIGNAME)
     preamble.set(buf.data() + t2sin.size);
     message.set(buf.data() + t2sin.size + preamble.size);
     message_with_preamble.set(buf.data() + t2sin.size);
+    ofdm_compat::Chain& ch = mirrors_->chain;
+    ch.pre_form = &preamble;
+    ch.msg_form = &message;
+    ch.mwp_form = &message_with_preamble;
+    ch.region = reinterpret_cast<char*>(buf.data() + t2sin.size);
+    ch.region_bytes = (size_t)message_with_preamble.size * CD;
+    ch.pre_bytes = (size_t)preamble.size * CD;
+    ch.chan_bytes = preamble.chan_est.size() * CD;
+    ch.cons_bytes = (size_t)message.usefull_size * CD;
+    ch.pre_ctx = preamble.ctx_;
+    ch.msg_ctx = message.ctx_;
+    ch.mwp_ctx = message_with_preamble.ctx_;
 }
 
 void FRAME_FORM::write(bit_vector& input) { message.write(input); }

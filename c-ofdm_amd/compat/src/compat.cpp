@@ -84,8 +84,20 @@ Context::Context(const ofdm_params& p) : params(p)
           "ofdm_get_preamble");
 }
 
+const int* Context::zero_index()
+{
+    if (!zero_) {
+        void* d = nullptr;
+        check(ofdm_device_alloc(ctx, sizeof(int), &d), "ofdm_device_alloc");
+        check(ofdm_memset_device(ctx, d, 0, sizeof(int), engine().stream), "ofdm_memset_device");
+        zero_ = static_cast<int*>(d);
+    }
+    return zero_;
+}
+
 Context::~Context()
 {
+    if (zero_) ofdm_device_free(ctx, zero_);
     for (auto& s : slots_)
         if (s.first) ofdm_device_free(ctx, s.first);
     ofdm_destroy(ctx);
@@ -151,12 +163,12 @@ void Engine::h2d(void* dev, const void* host, size_t bytes)
 
 void Engine::h2d_pinned(void* dev, const void* pinned, size_t bytes)
 {
-    if (bytes) check(ofdm_memcpy_h2d(ctx, dev, pinned, bytes, stream), "ofdm_memcpy_h2d");
+    if (bytes) check(ofdm_copy(ctx, dev, pinned, bytes, stream), "ofdm_copy");
 }
 
 void Engine::d2h_pinned(void* pinned, const void* dev, size_t bytes)
 {
-    if (bytes) check(ofdm_memcpy_d2h(ctx, pinned, dev, bytes, stream), "ofdm_memcpy_d2h");
+    if (bytes) check(ofdm_copy(ctx, pinned, dev, bytes, stream), "ofdm_copy");
 }
 
 void Engine::d2h(void* host, const void* dev, size_t bytes)
@@ -231,12 +243,22 @@ Mirror::~Mirror()
     ofdm_host_free(ctx->ctx, shadow);
 }
 
+void Mirror::settle()
+{
+    if (stale_lo == stale_hi) return;
+    ++gen;
+    ctx->engine().h2d_pinned(dev + stale_lo, shadow + stale_lo, stale_hi - stale_lo);
+    stale_lo = stale_hi = 0;
+}
+
 void Mirror::push(const void* p, size_t n)
 {
+    settle();
     const size_t off = static_cast<const char*>(p) - host;
     size_t lo, hi;
     diff_span(host + off, shadow + off, n, lo, hi);
     if (lo == hi) return;  // the device already holds these bytes
+    ++gen;
     std::memcpy(shadow + off + lo, host + off + lo, hi - lo);
     ctx->engine().h2d_pinned(dev + off + lo, shadow + off + lo, hi - lo);
 }
@@ -245,6 +267,7 @@ void Mirror::pull(const void* p, size_t n)
 {
     const size_t off = static_cast<const char*>(p) - host;
     Engine& e = ctx->engine();
+    ++gen;
     e.d2h_pinned(shadow + off, dev + off, n);
     e.sync();
     std::memcpy(host + off, shadow + off, n);
@@ -258,7 +281,89 @@ Mirror* find_mirror(const void* p, size_t n)
     return nullptr;
 }
 
-FrameMirrors::~FrameMirrors() = default;
+namespace {
+std::vector<FrameMirrors*> g_frames;  // guarded by g_mirror_mu
+}
+
+FrameMirrors::FrameMirrors()
+{
+    std::lock_guard<std::mutex> lock(g_mirror_mu);
+    g_frames.push_back(this);
+}
+
+FrameMirrors::~FrameMirrors()
+{
+    std::lock_guard<std::mutex> lock(g_mirror_mu);
+    g_frames.erase(std::remove(g_frames.begin(), g_frames.end(), this), g_frames.end());
+}
+
+Chain* chain_of(const void* form)
+{
+    std::lock_guard<std::mutex> lock(g_mirror_mu);
+    for (FrameMirrors* f : g_frames) {
+        Chain& c = f->chain;
+        if (form && (form == c.pre_form || form == c.msg_form || form == c.mwp_form)) return &c;
+    }
+    return nullptr;
+}
+
+size_t mirror_gen(const void* p, size_t n)
+{
+    Mirror* m = find_mirror(p, n);
+    return m ? m->gen : 0;
+}
+
+bool mirror_clean(const void* p, size_t n, size_t gen)
+{
+    Mirror* m = find_mirror(p, n);
+    if (!m || m->gen != gen) return false;
+    const size_t off = static_cast<const char*>(p) - m->host;
+    size_t lo, hi;
+    diff_span(m->host + off, m->shadow + off, n, lo, hi);
+    return lo == hi;
+}
+
+Chain::~Chain()
+{
+    if (!mwp_ctx) return;
+    ofdm_ctx* c = mwp_ctx->ctx;
+    for (int i = 0; i < 3; ++i) {
+        if (hstate[i]) ofdm_host_free(c, hstate[i]);
+    }
+    for (void* d : {(void*)dchan, (void*)dcons, (void*)dcfo})
+        if (d) ofdm_device_free(c, d);
+    for (void* h : {(void*)hchan, (void*)hcons, (void*)hcfo})
+        if (h) ofdm_host_free(c, h);
+    for (void* e : ev)
+        if (e) ofdm_event_destroy(c, e);
+}
+
+bool Chain::alloc(Engine& e)
+{
+    (void)e;
+    if (dcfo) return true;
+    if (!mwp_ctx || !region) return false;
+    ofdm_ctx* c = mwp_ctx->ctx;
+    void* p = nullptr;
+    for (int i = 0; i < 3; ++i) {
+        check(ofdm_host_alloc(c, region_bytes, &p), "ofdm_host_alloc");
+        hstate[i] = static_cast<char*>(p);
+    }
+    check(ofdm_device_alloc(c, chan_bytes, &p), "ofdm_device_alloc");
+    dchan = static_cast<char*>(p);
+    check(ofdm_host_alloc(c, chan_bytes, &p), "ofdm_host_alloc");
+    hchan = static_cast<char*>(p);
+    check(ofdm_device_alloc(c, cons_bytes, &p), "ofdm_device_alloc");
+    dcons = static_cast<char*>(p);
+    check(ofdm_host_alloc(c, cons_bytes, &p), "ofdm_host_alloc");
+    hcons = static_cast<char*>(p);
+    check(ofdm_host_alloc(c, sizeof(double), &p), "ofdm_host_alloc");
+    hcfo = static_cast<double*>(p);
+    for (auto& v : ev) check(ofdm_event_create(c, &v), "ofdm_event_create");
+    check(ofdm_device_alloc(c, sizeof(double), &p), "ofdm_device_alloc");
+    dcfo = static_cast<double*>(p);
+    return true;
+}
 
 void FrameMirrors::add(std::shared_ptr<Context> c, void* host, size_t bytes)
 {

@@ -152,6 +152,7 @@ struct ofdm_ctx {
         size_t bytes = 0;
     };
     Grow s_walk, s_batch, s_chan, s_pbs;
+    Grow s_pre, s_pre_done;  // find_preamble: split magnitudes, per-start counters (zero between launches)
     // pinned host staging for the walk records and the frame list (pageable
     // copies go through a driver bounce buffer and synchronise twice)
     Grow h_walk, h_frames;
@@ -315,7 +316,7 @@ int ofdm_destroy(ofdm_ctx* c)
                     c->d_t2tw, c->d_first, c->d_scratch, c->d_cfo_scratch};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
-    for (auto* g : {&c->s_walk, &c->s_batch, &c->s_chan, &c->s_pbs})
+    for (auto* g : {&c->s_walk, &c->s_batch, &c->s_chan, &c->s_pbs, &c->s_pre, &c->s_pre_done})
         if (g->p) (void)hipFree(g->p);
     for (auto* g : {&c->h_walk, &c->h_frames})
         if (g->p) (void)hipHostFree(g->p);
@@ -570,7 +571,9 @@ int ofdm_create(const ofdm_params* params, int device, ofdm_ctx** out)
         }
     }
     // T2 detector tables
-    if ((rc = upload(&c->d_first, std::vector<int>(4, 0)))) {
+    // T2 detector scratch {min block = INT_MAX, done count = 0} (left so by
+    // every t2_scan launch), word 2: preamble_corr's start index
+    if ((rc = upload(&c->d_first, std::vector<int>{INT_MAX, 0, 0, 0}))) {
         ofdm_destroy(c);
         return rc;
     }
@@ -744,6 +747,47 @@ int ofdm_stream_destroy(ofdm_ctx* c, void* st)
 {
     if (!c) return fail(OFDM_ERR_INVALID, "null ctx");
     if (st) HIP_TRY(hipStreamDestroy((hipStream_t)st));
+    return OFDM_OK;
+}
+int ofdm_memcpy_d2d(ofdm_ctx* c, void* dst, const void* src, size_t n, void* st)
+{
+    if (!c) return fail(OFDM_ERR_INVALID, "null ctx");
+    if (n) HIP_TRY(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, (hipStream_t)st));
+    return OFDM_OK;
+}
+int ofdm_copy(ofdm_ctx* c, void* dst, const void* src, size_t n, void* st)
+{
+    if (!c) return fail(OFDM_ERR_INVALID, "null ctx");
+    if (n && (!dst || !src)) return fail(OFDM_ERR_INVALID, "null argument");
+    hipError_t e = ofdm::launch_copy(dst, src, n, (hipStream_t)st);
+    if (e != hipSuccess) return hip_fail(e, "copy launch");
+    return OFDM_OK;
+}
+int ofdm_event_create(ofdm_ctx* c, void** ev)
+{
+    if (!c || !ev) return fail(OFDM_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    hipEvent_t e = nullptr;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    *ev = e;
+    return OFDM_OK;
+}
+int ofdm_event_record(ofdm_ctx* c, void* ev, void* st)
+{
+    if (!c || !ev) return fail(OFDM_ERR_INVALID, "null argument");
+    HIP_TRY(hipEventRecord((hipEvent_t)ev, (hipStream_t)st));
+    return OFDM_OK;
+}
+int ofdm_event_synchronize(ofdm_ctx* c, void* ev)
+{
+    if (!c || !ev) return fail(OFDM_ERR_INVALID, "null argument");
+    HIP_TRY(hipEventSynchronize((hipEvent_t)ev));
+    return OFDM_OK;
+}
+int ofdm_event_destroy(ofdm_ctx* c, void* ev)
+{
+    if (!c) return fail(OFDM_ERR_INVALID, "null ctx");
+    if (ev) HIP_TRY(hipEventDestroy((hipEvent_t)ev));
     return OFDM_OK;
 }
 
@@ -1031,6 +1075,21 @@ int ofdm_t2_scan(ofdm_ctx* c, const double* iq, size_t n, long start, double* re
     return OFDM_OK;
 }
 
+// Scratch of a find_preamble launch over nstarts start indices.
+static int preamble_scratch(ofdm_ctx* c, size_t nstarts, ofdm::PreambleArgs& a)
+{
+    if (ofdm::preamble_splits(a.cycles) <= 1) return OFDM_OK;
+    int rc;
+    if ((rc = grow(c, c->s_pre, nstarts * a.cycles * sizeof(double)))) return rc;
+    if (nstarts * sizeof(unsigned) > c->s_pre_done.bytes) {
+        if ((rc = grow(c, c->s_pre_done, nstarts * sizeof(unsigned)))) return rc;
+        HIP_TRY(hipMemset(c->s_pre_done.p, 0, c->s_pre_done.bytes));
+    }
+    a.hv_scratch = static_cast<double*>(c->s_pre.p);
+    a.done = static_cast<unsigned*>(c->s_pre_done.p);
+    return OFDM_OK;
+}
+
 int ofdm_find_preamble(ofdm_ctx* c, const double* iq, size_t n, const int* starts, size_t nstarts, int* idx_out,
                        void* stream)
 {
@@ -1046,6 +1105,7 @@ int ofdm_find_preamble(ofdm_ctx* c, const double* iq, size_t n, const int* start
     a.L = (int)c->p.pr_sin_len;
     a.cycles = (int)(2 * c->p.t2sin_size + c->p.pr_sin_len);
     a.level = (double)c->p.pr_level / 1000;
+    if (int rc = preamble_scratch(c, nstarts, a)) return rc;
     hipError_t e = ofdm::launch_find_preamble(a, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "find_preamble launch");
     return OFDM_OK;
@@ -1070,6 +1130,7 @@ int ofdm_preamble_corr(ofdm_ctx* c, const double* iq, size_t n, long start, doub
     a.cycles = (int)(2 * c->p.t2sin_size + c->p.pr_sin_len);
     a.level = (double)c->p.pr_level / 1000;
     a.cor_out = cor_out;
+    if (int rc = preamble_scratch(c, 1, a)) return rc;
     hipError_t e = ofdm::launch_find_preamble(a, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "preamble_corr launch");
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));  // the start word is host-staged

@@ -72,6 +72,7 @@ struct RxArgs {
 // Launchers (ofdm_kernels.hip). Return hipSuccess or the launch error.
 hipError_t launch_tx(int logn, const TxArgs& a, hipStream_t stream);
 hipError_t launch_rx(int logn, const RxArgs& a, hipStream_t stream, bool* staged_needed);
+hipError_t launch_copy(void* dst, const void* src, size_t n, hipStream_t stream);  // kernel copy (device / mapped pinned)
 hipError_t launch_demap(double2* pts, long n, int k, uint8_t* bytes, hipStream_t stream);
 hipError_t launch_map(const uint8_t* bytes, long nbytes, int k, const double2* table, double2* out,
                       hipStream_t stream);

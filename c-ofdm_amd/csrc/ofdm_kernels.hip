@@ -15,6 +15,7 @@
 //                 VGPRs until the frame-global pilot normalisation is known.
 //   demap/map   : Modulation::demod / ::mod on flat point arrays.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 
@@ -1116,6 +1117,39 @@ hipError_t launch_i16_to_f64(const int16_t* in, long n, double* out, hipStream_t
     if (grid > 8192) grid = 8192;
     hipLaunchKernelGGL(i16_to_f64_kernel, dim3((unsigned)grid), dim3(256), 0, st, reinterpret_cast<const short2*>(in), n,
                        reinterpret_cast<double2*>(out));
+    return hipGetLastError();
+}
+
+// Copy by a kernel on the stream's compute queue: device memory or mapped
+// page-locked host memory on either side. Small transfers between kernels
+// then need no hand-off to a DMA engine and back (each such hand-off costs
+// several microseconds of queue synchronisation).
+__global__ void __launch_bounds__(256) copy16_kernel(uint4* dst, const uint4* src, long n16, char* dtail,
+                                                     const char* stail, int ntail)
+{
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n16; i += (long)gridDim.x * 256) dst[i] = src[i];
+    if (blockIdx.x == 0 && threadIdx.x < ntail) dtail[threadIdx.x] = stail[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(256) copy1_kernel(char* dst, const char* src, long n)
+{
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) dst[i] = src[i];
+}
+
+hipError_t launch_copy(void* dst, const void* src, size_t n, hipStream_t st)
+{
+    if (!n) return hipSuccess;
+    char* d = static_cast<char*>(dst);
+    const char* s = static_cast<const char*>(src);
+    if ((((uintptr_t)d | (uintptr_t)s) & 15) == 0) {
+        const long n16 = (long)(n / 16);
+        const long grid = std::max(1L, std::min((n16 + 255) / 256, 2048L));
+        hipLaunchKernelGGL(copy16_kernel, dim3((unsigned)grid), dim3(256), 0, st, reinterpret_cast<uint4*>(d),
+                           reinterpret_cast<const uint4*>(s), n16, d + n16 * 16, s + n16 * 16, (int)(n % 16));
+    } else {
+        const long grid = std::min(((long)n + 255) / 256, 2048L);
+        hipLaunchKernelGGL(copy1_kernel, dim3((unsigned)grid), dim3(256), 0, st, d, s, (long)n);
+    }
     return hipGetLastError();
 }
 

@@ -233,6 +233,18 @@ __global__ void __launch_bounds__(T2Geo<LOGN>::NT) t2_scan_kernel(T2Args a)
         }
         if (a.rel_out) a.rel_out[b] = out;
     }
+    // the last workgroup to finish turns the minimum into find_t2sin's answer
+    // and leaves the scratch {INT_MAX, 0} for the next launch (one launch per
+    // call: no reset or finalize launches around it)
+    __syncthreads();
+    if (tid == 0) {
+        __threadfence();
+        if (atomicAdd(a.first_scratch + 1, 1) == (int)gridDim.x - 1) {
+            const int m = atomicExch(a.first_scratch, INT_MAX);
+            if (a.first_out) *a.first_out = m == INT_MAX ? -1 : (int)(a.start + (long)m * N);
+            atomicExch(a.first_scratch + 1, 0);
+        }
+    }
 }
 
 __global__ void t2_finalize_kernel(const int* scratch, int* first_out, long start, int size)
@@ -252,13 +264,10 @@ static hipError_t t2_launch_n(const T2Args& a, hipStream_t st)
     return hipGetLastError();
 }
 
-hipError_t launch_t2_scan(int logn, const T2Args& a, int* first_out, hipStream_t st)
+hipError_t launch_t2_scan(int logn, const T2Args& a0, int* first_out, hipStream_t st)
 {
-    if (a.first_scratch) {
-        const int big = INT_MAX;
-        hipError_t e = hipMemsetD32Async((hipDeviceptr_t)a.first_scratch, big, 1, st);
-        if (e != hipSuccess) return e;
-    }
+    T2Args a = a0;
+    a.first_out = first_out;
     hipError_t e = hipSuccess;
     if (a.nblocks > 0) {
         switch (logn) {
@@ -273,7 +282,7 @@ hipError_t launch_t2_scan(int logn, const T2Args& a, int* first_out, hipStream_t
         }
     }
     if (e != hipSuccess) return e;
-    if (first_out) {
+    if (first_out && a.nblocks <= 0) {  // no block to scan: -1 (the scratch holds INT_MAX)
         hipLaunchKernelGGL(t2_finalize_kernel, dim3(1), dim3(1), 0, st, a.first_scratch, first_out, a.start,
                            1 << logn);
         e = hipGetLastError();
@@ -282,78 +291,224 @@ hipError_t launch_t2_scan(int logn, const T2Args& a, int* first_out, hipStream_t
 }
 
 // ========================================================================
-// Preamble detector: one workgroup per start index.
+// Preamble detector: per start index, ceil(C / PRE_THREADS) workgroups each
+// correlate PRE_THREADS lags (one per thread); the last of them to finish
+// (a per-start counter) gathers the magnitudes and runs the screen and the
+// serial energy recurrence.
 // ========================================================================
-__global__ void __launch_bounds__(SYNC_THREADS) find_preamble_kernel(PreambleArgs a)
+constexpr int PRE_THREADS = 256;
+constexpr int PRE_BATCH = 16;  // serial recurrence: energies fetched 16 at a time
+
+__global__ void __launch_bounds__(PRE_THREADS) find_preamble_kernel(PreambleArgs a)
 {
     extern __shared__ double2 smem[];
-    const int L = a.L, C = a.cycles;
-    double2* xs = smem;                      // C + L samples
-    double2* c = xs + C + L;                 // L template taps
-    double* normv = reinterpret_cast<double*>(c + L);  // C running energies
-    int* best = reinterpret_cast<int*>(normv + C);
-    const int t = threadIdx.x;
-    const long s = a.starts[blockIdx.x];
-    for (int i = t; i < C + L; i += SYNC_THREADS) {
-        const long j = s + i;
-        xs[i] = (j >= 0 && j < a.n) ? a.iq[j] : make_double2(0.0, 0.0);
-    }
-    for (int i = t; i < L; i += SYNC_THREADS) c[i] = a.templ[i];
-    if (t == 0) *best = INT_MAX;
-    __syncthreads();
-    // serial running energy, exactly the reference's operation order (Frame.cpp:346-375)
-    if (t == 0) {
-        double norm = 0.0;
-        for (int i = 0; i < L; ++i) norm = add_rn(norm, add_rn(mul_rn(xs[i].x, xs[i].x), mul_rn(xs[i].y, xs[i].y)));
-        for (int i = 0; i < C; ++i) {
-            normv[i] = norm;
-            const double2 p = xs[i + L], q = xs[i];
-            norm = add_rn(norm, add_rn(mul_rn(p.x, p.x), mul_rn(p.y, p.y)));
-            norm = sub_rn(norm, add_rn(mul_rn(q.x, q.x), mul_rn(q.y, q.y)));
+    const int L = a.L, C = a.cycles, n = C + L;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const long s = a.starts[blockIdx.y];
+    const int nsplit = gridDim.x, lag0 = blockIdx.x * PRE_THREADS, cnt = min(PRE_THREADS, C - lag0);
+    int& last_block = *reinterpret_cast<int*>(smem);  // (dynamic LDS only: the opt-in takes all 160 KB)
+    double* hv = reinterpret_cast<double*>(smem + 1);  // C correlation magnitudes
+    {
+        double2* xs = reinterpret_cast<double2*>(hv + C);  // this slice's cnt + L samples
+        for (int i = t; i < cnt + L; i += PRE_THREADS) {
+            const long j = s + lag0 + i;
+            xs[i] = (j >= 0 && j < a.n) ? a.iq[j] : make_double2(0.0, 0.0);
+        }
+        __syncthreads();
+        // correlation per lag, j = 0..L-1 in order (Frame.cpp:360-363), and its magnitude
+        if (t < cnt) {
+            double2 e = make_double2(0.0, 0.0);
+            int j = 0;
+            for (; j + 8 <= L; j += 8) {  // operands a batch ahead: the chain waits on its adds alone
+                double2 xv[8], cv[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    xv[k] = xs[t + j + k];
+                    cv[k] = a.templ[j + k];
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k) e = cadd_rn(e, cmul_exact(xv[k], cv[k]));
+            }
+            for (; j < L; ++j) e = cadd_rn(e, cmul_exact(xs[t + j], a.templ[j]));
+            const double h = hypot(e.x, e.y);
+            hv[lag0 + t] = h;
+            if (nsplit > 1) a.hv_scratch[blockIdx.y * (long)C + lag0 + t] = h;
+        }
+        if (nsplit > 1) {
+            __threadfence();  // release this slice
+            __syncthreads();
+            if (t == 0) last_block = atomicAdd(a.done + blockIdx.y, 1u) == (unsigned)nsplit - 1;
+            __syncthreads();
+            if (!last_block) return;
+            __threadfence();  // acquire the other slices
+            for (int i = t; i < C; i += PRE_THREADS)
+                if (i - lag0 < 0 || i - lag0 >= cnt) hv[i] = a.hv_scratch[blockIdx.y * (long)C + i];
+            if (t == 0) a.done[blockIdx.y] = 0u;  // zero between launches
         }
     }
-    // correlation per lag, j = 0..L-1 in order (Frame.cpp:360-363)
-    double2 en[4];
-    int nl = 0;
-    for (int i = t; i < C && nl < 4; i += SYNC_THREADS, ++nl) {
-        double2 e = make_double2(0.0, 0.0);
-        for (int j = 0; j < L; ++j) e = cadd_rn(e, cmul_exact(xs[i + j], c[j]));
-        en[nl] = e;
+    double* en = hv + C;                     // C + L sample energies
+    double* ps = en + n;                     // C + L + 1 prefix sums of en (ps[k] = sum en[0..k))
+    double* normv = ps + n + 1;              // C + PRE_BATCH running energies
+    double* wsum = normv + C + PRE_BATCH;    // PRE_THREADS / 64 wave totals
+    int* best = reinterpret_cast<int*>(wsum + PRE_THREADS / 64);
+    int* lastc = best + 1;
+    unsigned* cand = reinterpret_cast<unsigned*>(best + 2);  // C bits: lags whose test can pass
+    __syncthreads();  // the slice's samples are dead: en overlays them
+    for (int i = t; i < n; i += PRE_THREADS) {
+        const long j = s + i;
+        const double2 v = (j >= 0 && j < a.n) ? a.iq[j] : make_double2(0.0, 0.0);
+        en[i] = add_rn(mul_rn(v.x, v.x), mul_rn(v.y, v.y));  // |x|^2 as the reference rounds it
+    }
+    for (int i = t; i < (C + 31) / 32; i += PRE_THREADS) cand[i] = 0u;
+    if (t == 0) {
+        *best = INT_MAX;
+        *lastc = -1;
     }
     __syncthreads();
-    double* cor = a.cor_out ? a.cor_out + (long)blockIdx.x * C : nullptr;
-    nl = 0;
-    for (int i = t; i < C && nl < 4; i += SYNC_THREADS, ++nl) {
-        const double norm = normv[i];
-        const double r = norm > 1.0 ? hypot(en[nl].x, en[nl].y) / sqrt(norm) : 0.0;
-        if (cor) cor[i] = r;
-        if (norm > 1.0 && r > a.level) atomicMin(best, i);
-    }
-    // lags beyond 4*SYNC_THREADS (C > 1024): continue serially in chunks
-    for (int base = 4 * SYNC_THREADS; base < C; base += SYNC_THREADS) {
-        const int i = base + t;
-        if (i < C) {
-            double2 e = make_double2(0.0, 0.0);
-            for (int j = 0; j < L; ++j) e = cadd_rn(e, cmul_exact(xs[i + j], c[j]));
+    if (a.cor_out) {
+        // find_corr: every lag's value, so the whole serial recurrence
+        if (t == 0) {
+            double norm = 0.0;
+            for (int i = 0; i < L; ++i) norm = add_rn(norm, en[i]);
+            for (int i = 0; i < C; ++i) {
+                normv[i] = norm;
+                norm = add_rn(norm, en[i + L]);
+                norm = sub_rn(norm, en[i]);
+            }
+        }
+        __syncthreads();
+        double* cor = a.cor_out + (long)blockIdx.y * C;
+        for (int i = t; i < C; i += PRE_THREADS) {
             const double norm = normv[i];
-            const double r = norm > 1.0 ? hypot(e.x, e.y) / sqrt(norm) : 0.0;
-            if (cor) cor[i] = r;
+            const double r = norm > 1.0 ? hv[i] / sqrt(norm) : 0.0;
+            cor[i] = r;
             if (norm > 1.0 && r > a.level) atomicMin(best, i);
         }
+        __syncthreads();
+        if (t == 0 && a.idx_out) a.idx_out[blockIdx.y] = *best == INT_MAX ? -10 : (int)(s + *best);
+        return;
+    }
+    // Certified screen. The reference's running energy norm_i (Frame.cpp:346-375:
+    // +|x[i+L]|^2 - |x[i]|^2 after each test) is L - 1 + 2i rounded adds /
+    // subs of nonnegative energies, each erring by at most u (2^-53) of a
+    // partial sum <= P[i+L]; the window sum W_i = ps[i+L] - ps[i] of the
+    // parallel prefix sum (a serial run per thread, a wave scan, the wave
+    // totals: fewer than n + 2 PRE_THREADS rounded adds on any path) errs by at
+    // most 2 (n + 2 PRE_THREADS) u P[n] + u |W_i|. b_i is twice their sum. A
+    // lag is a candidate when its test (norm > 1, |corr| / sqrt(norm) > level;
+    // sqrt and division round by u each) can pass for a norm within b_i of
+    // W_i; the others certainly fail. The exact serial recurrence then runs
+    // only up to the first candidate that passes (or the last candidate),
+    // testing the candidates alone.
+    {
+        const int per = (n + PRE_THREADS - 1) / PRE_THREADS, lo = min(n, t * per), hi = min(n, lo + per);
+        double run = 0.0;
+        for (int i = lo; i < hi; ++i) run += en[i];
+        double inc = run;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const double y = __shfl_up(inc, o);
+            if (lane >= o) inc += y;
+        }
+        if (lane == 63) wsum[w] = inc;
+        __syncthreads();
+        double acc = inc - run;  // exclusive within the wave (any rounding: covered by the bound)
+        for (int k = 0; k < w; ++k) acc += wsum[k];
+        for (int i = lo; i < hi; ++i) {
+            acc += en[i];
+            ps[i + 1] = acc;
+        }
+        if (t == 0) ps[0] = 0.0;
+        __syncthreads();
+        constexpr double u = 0x1.0p-53;
+        const double total = ps[n];
+        const double lev2 = a.level * a.level;
+        for (int i = t; i < C; i += PRE_THREADS) {
+            const double wi = ps[i + L] - ps[i];
+            const double b = 2.0 * u * ((L + 2.0 * i + 2.0) * ps[i + L] + 2.0 * (n + 2.0 * PRE_THREADS) * total) +
+                             4.0 * u * fabs(wi);
+            const double hmax = hv[i] * (1.0 + 8.0 * u);
+            const bool can = !isnan(hv[i]) && wi + b > 1.0 && hmax * hmax * (1.0 + 8.0 * u) > lev2 * fmax(wi - b, 1.0);
+            if (can) {
+                atomicOr(&cand[i >> 5], 1u << (i & 31));
+                atomicMax(lastc, i);
+            }
+        }
     }
     __syncthreads();
-    if (t == 0 && a.idx_out) a.idx_out[blockIdx.x] = *best == INT_MAX ? -10 : (int)(s + *best);
+    // the reference's serial recurrence, up to the first passing candidate.
+    // A batch of PRE_BATCH steps is straight-line code on energies fetched
+    // ahead (the chain waits on its adds alone); a batch holding candidates
+    // keeps each step's norm and tests them afterwards, in order. Steps past
+    // `last` read beyond the energies (into ps) and are never tested.
+    if (t == 0) {
+        const int last = *lastc;
+        double norm = 0.0;
+        int i0 = 0;
+        for (; i0 + PRE_BATCH <= L; i0 += PRE_BATCH) {
+            double v[PRE_BATCH];
+#pragma unroll
+            for (int k = 0; k < PRE_BATCH; ++k) v[k] = en[i0 + k];
+#pragma unroll
+            for (int k = 0; k < PRE_BATCH; ++k) norm = add_rn(norm, v[k]);
+        }
+        for (; i0 < L; ++i0) norm = add_rn(norm, en[i0]);
+        int found = INT_MAX;
+        for (int b0 = 0; b0 <= last && found == INT_MAX; b0 += PRE_BATCH) {
+            double in[PRE_BATCH], out[PRE_BATCH];
+#pragma unroll
+            for (int k = 0; k < PRE_BATCH; ++k) {
+                in[k] = en[b0 + k + L];
+                out[k] = en[b0 + k];
+            }
+            unsigned bits = (cand[b0 >> 5] >> (b0 & 31)) & ((1u << PRE_BATCH) - 1u);  // PRE_BATCH divides 32
+            if (bits) {
+#pragma unroll
+                for (int k = 0; k < PRE_BATCH; ++k) {
+                    normv[b0 + k] = norm;
+                    norm = add_rn(norm, in[k]);
+                    norm = sub_rn(norm, out[k]);
+                }
+                for (; bits; bits &= bits - 1u) {
+                    const int i = b0 + __builtin_ctz(bits);
+                    const double nv = normv[i];
+                    if (nv > 1.0 && hv[i] / sqrt(nv) > a.level) {
+                        found = i;
+                        break;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < PRE_BATCH; ++k) {
+                    norm = add_rn(norm, in[k]);
+                    norm = sub_rn(norm, out[k]);
+                }
+            }
+        }
+        *best = found;
+    }
+    __syncthreads();
+    if (t == 0 && a.idx_out) a.idx_out[blockIdx.y] = *best == INT_MAX ? -10 : (int)(s + *best);
 }
 
 hipError_t launch_find_preamble(const PreambleArgs& a, hipStream_t st)
 {
     if (a.nstarts <= 0) return hipSuccess;
-    const size_t shm = sizeof(double2) * (a.cycles + 2 * (size_t)a.L) + sizeof(double) * a.cycles + 16;
+    const int nsplit = preamble_splits(a.cycles);
+    if (nsplit > 1 && (!a.hv_scratch || !a.done)) return hipErrorInvalidValue;
+    if (a.nstarts > 65535) return hipErrorInvalidValue;
+    const size_t C = (size_t)a.cycles, nn = C + a.L;
+    const size_t corr = sizeof(double) * C + sizeof(double2) * (std::min<size_t>(C, PRE_THREADS) + a.L);
+    const size_t tail = sizeof(double) * (C + nn + nn + 1 + C + PRE_BATCH + PRE_THREADS / 64) + sizeof(int) * 2 +
+                        sizeof(unsigned) * ((C + 31) / 32) + 64;
+    const size_t shm = sizeof(double2) + std::max(corr, tail);
     if (shm > 160 * 1024) return hipErrorInvalidValue;
     lds_opt_in((const void*)find_preamble_kernel, 160 * 1024);
-    hipLaunchKernelGGL(find_preamble_kernel, dim3((unsigned)a.nstarts), dim3(SYNC_THREADS), shm, st, a);
+    hipLaunchKernelGGL(find_preamble_kernel, dim3((unsigned)nsplit, (unsigned)a.nstarts), dim3(PRE_THREADS), shm, st, a);
     return hipGetLastError();
 }
+
+int preamble_splits(int cycles) { return (cycles + PRE_THREADS - 1) / PRE_THREADS; }
 
 // ========================================================================
 // pilot_freq_sinh: FFT of the whole form (M or 5*M points, M = 2^LOGM) as G
@@ -548,26 +703,41 @@ hipError_t launch_freq_shift(const ShiftArgs& a, hipStream_t st)
 // cp_freq_sinh: phi_s = arg sum_{j<cp} conj(x[sL+j]) x[sL+j+N];
 // sample (s, j) *= exp(-i (sum_{q<s} phi_q * L + phi_s * j) / N)
 // ========================================================================
-__global__ void __launch_bounds__(SYNC_THREADS) cp_sync_kernel(CpArgs a)
+// One 1024-thread workgroup per frame: wave w correlates the CP of symbols
+// w, w + 16, ... (wave-level sums, no workgroup barrier per symbol), then the
+// phase prefix once, then the correction of every sample.
+constexpr int CP_THREADS = 1024;
+
+__global__ void __launch_bounds__(CP_THREADS) cp_sync_kernel(CpArgs a)
 {
-    __shared__ double2 red[SYNC_THREADS / 64];
     __shared__ double phi[64];
+    __shared__ double psi[64];
     const long f = blockIdx.x;
     double2* x = a.x + f * a.frame_stride;
-    const int t = threadIdx.x, L = a.N + a.cp;
-    for (int s = 0; s < a.nsym; ++s) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, L = a.N + a.cp;
+    for (int s = w; s < a.nsym; s += CP_THREADS / 64) {
         double2 acc = make_double2(0.0, 0.0);
-        for (int j = t; j < a.cp; j += SYNC_THREADS) acc = cadd(acc, cconj_mul(x[(long)s * L + j], x[(long)s * L + j + a.N]));
-        acc = block_sum2<SYNC_THREADS>(acc, red);
-        if (t == 0) phi[s] = atan2(acc.y, acc.x);
-        __syncthreads();
+        for (int j = lane; j < a.cp; j += 64) acc = cadd(acc, cconj_mul(x[(long)s * L + j], x[(long)s * L + j + a.N]));
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            acc.x += __shfl_xor(acc.x, o);
+            acc.y += __shfl_xor(acc.y, o);
+        }
+        if (lane == 0) phi[s] = atan2(acc.y, acc.x);
     }
+    __syncthreads();
+    if (t == 0) {  // psi_s = phi_0 + ... + phi_{s-1}, in that order (Frame.hpp:257-260)
+        double p = 0.0;
+        for (int q = 0; q < a.nsym; ++q) {
+            psi[q] = p;
+            p += phi[q];
+        }
+    }
+    __syncthreads();
     const long total = (long)a.nsym * L;
-    for (long n = t; n < total; n += SYNC_THREADS) {
+    for (long n = t; n < total; n += CP_THREADS) {
         const int s = (int)(n / L), j = (int)(n - (long)s * L);
-        double psi = 0.0;
-        for (int q = 0; q < s; ++q) psi += phi[q];
-        const double th = -(psi * L + phi[s] * j) / a.N;
+        const double th = -(psi[s] * L + phi[s] * j) / a.N;
         double sn, cs;
         sincos(th, &sn, &cs);
         x[n] = cmul(x[n], make_double2(cs, sn));
@@ -578,7 +748,7 @@ hipError_t launch_cp_sync(const CpArgs& a, hipStream_t st)
 {
     if (a.nframes <= 0) return hipSuccess;
     if (a.nsym > 64) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(cp_sync_kernel, dim3((unsigned)a.nframes), dim3(SYNC_THREADS), 0, st, a);
+    hipLaunchKernelGGL(cp_sync_kernel, dim3((unsigned)a.nframes), dim3(CP_THREADS), 0, st, a);
     return hipGetLastError();
 }
 
@@ -1049,7 +1219,6 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
     double2* dat = Ls.dat;
     double2* red = Ls.red;
     double2* cps = Ls.cps;
-    double* amp = Ls.amp;
     double* ph = Ls.ph;
     double* phi = Ls.phi;
     double* psi = Ls.psi;

@@ -15,7 +15,8 @@ struct T2Args {
     int a1, b1, a2, b2;     // detector mask bands (Frame.cpp:120-133)
     double level;           // T2_sin_level / 1000
     double* rel_out;        // nullable: nblocks ratios (0 where <= level)
-    int* first_scratch;     // device int, min block index above level
+    int* first_scratch;     // device {min block index above level (INT_MAX between launches), done count (0)}
+    int* first_out;         // nullable: find_t2sin's answer, written by the last workgroup
 };
 
 struct PreambleArgs {
@@ -29,6 +30,8 @@ struct PreambleArgs {
     int cycles;             // 2*T2sin_size + pr_sin_len
     double level;           // pr_level / 1000
     double* cor_out;        // nullable: find_corr values, cycles per start
+    double* hv_scratch;     // nstarts * cycles (when preamble_splits(cycles) > 1)
+    unsigned* done;         // nstarts counters, zero between launches (idem)
 };
 
 struct CfoArgs {
@@ -181,6 +184,7 @@ long stream_walk_slots(int logt, int L, int C, bool fft);
 hipError_t launch_gather(const GatherArgs& a, hipStream_t st);
 hipError_t launch_t2_scan(int logn, const T2Args& a, int* first_out, hipStream_t st);
 hipError_t launch_find_preamble(const PreambleArgs& a, hipStream_t st);
+int preamble_splits(int cycles);  // workgroups per start index
 hipError_t launch_cfo(int logm, int g, const CfoArgs& a, hipStream_t st);
 hipError_t launch_freq_shift(const ShiftArgs& a, hipStream_t st);
 hipError_t launch_cp_sync(const CpArgs& a, hipStream_t st);

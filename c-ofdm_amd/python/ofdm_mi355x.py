@@ -84,6 +84,7 @@ SIGNATURES = {
     "ofdm_device_free": (_I, [_V, _V]),
     "ofdm_memcpy_h2d": (_I, [_V, _V, _V, _SZ, _V]),
     "ofdm_memcpy_d2h": (_I, [_V, _V, _V, _SZ, _V]),
+    "ofdm_copy": (_I, [_V, _V, _V, _SZ, _V]),
     "ofdm_memset_device": (_I, [_V, _V, _I, _SZ, _V]),
     "ofdm_stream_synchronize": (_I, [_V, _V]),
     "ofdm_tx_modulate": (_I, [_V, _V, _SZ, _V, _SZ, _V, C.POINTER(Channel), _V]),
@@ -115,6 +116,11 @@ SIGNATURES = {
     "ofdm_host_free": (_I, [_V, _V]),
     "ofdm_stream_create": (_I, [_V, C.POINTER(_V)]),
     "ofdm_stream_destroy": (_I, [_V, _V]),
+    "ofdm_memcpy_d2d": (_I, [_V, _V, _V, _SZ, _V]),
+    "ofdm_event_create": (_I, [_V, C.POINTER(_V)]),
+    "ofdm_event_record": (_I, [_V, _V, _V]),
+    "ofdm_event_synchronize": (_I, [_V, _V]),
+    "ofdm_event_destroy": (_I, [_V, _V]),
     "ofdm_walk_tuning_default": (_I, [C.POINTER(WalkTuning)]),
     "ofdm_get_walk_tuning": (_I, [_V, C.POINTER(WalkTuning)]),
     "ofdm_set_walk_tuning": (_I, [_V, C.POINTER(WalkTuning)]),

@@ -139,6 +139,18 @@ int ofdm_host_free(ofdm_ctx* ctx, void* hptr);
 /* A non-blocking HIP stream on the ctx's device, and its destruction. */
 int ofdm_stream_create(ofdm_ctx* ctx, void** stream);
 int ofdm_stream_destroy(ofdm_ctx* ctx, void* stream);
+/* Device-to-device copy on a stream; HIP events (timing disabled) to wait
+ * for part of a stream's work. */
+int ofdm_memcpy_d2d(ofdm_ctx* ctx, void* dst, const void* src, size_t bytes, void* stream);
+/* Copy by a kernel on the stream (no DMA engine): dst and src each device
+ * memory or page-locked host memory from ofdm_host_alloc. For the small
+ * transfers between a stream's kernels, where a DMA hand-off costs more than
+ * the copy. */
+int ofdm_copy(ofdm_ctx* ctx, void* dst, const void* src, size_t bytes, void* stream);
+int ofdm_event_create(ofdm_ctx* ctx, void** event);
+int ofdm_event_record(ofdm_ctx* ctx, void* event, void* stream);
+int ofdm_event_synchronize(ofdm_ctx* ctx, void* event);
+int ofdm_event_destroy(ofdm_ctx* ctx, void* event);
 
 /* ---- tx: FRAME_FORM::write (Frame.cpp:235-237) -> OFDM_FORM::write
  *      (Frame.cpp:185-198) -> Modulation::mod (modulation.cpp:39-50) +

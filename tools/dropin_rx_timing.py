@@ -64,6 +64,8 @@ def gapped_capture(txf, frame_len, seed=4, gap_max=3000):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=200)
+    ap.add_argument("--trace", action="store_true",
+                    help="OFDM_COMPAT_TRACE=1: median wall time of each compat member call (diagnostics)")
     args = ap.parse_args()
     from test_dropin_gpu import D, O, write_config
     g = O.geometry(D)
@@ -79,7 +81,14 @@ def main():
         assert r.returncode == 0, r.stderr[-2000:]
         gapped_capture(txf, g["frame_len"])
         env = dict(os.environ, OFDM_SDR_RX_FILE=txf)
+        if args.trace:
+            env["OFDM_COMPAT_TRACE"] = "1"
         r = subprocess.run([os.path.join(REF_BIN, "rx")], cwd=d, env=env, capture_output=True, text=True, timeout=300)
+        calls = {}
+        for ln in r.stderr.splitlines():
+            m = re.match(r"\[compat\] (\S+) ([0-9.]+)$", ln)
+            if m:
+                calls.setdefault(m.group(1), []).append(float(m.group(2)))
         assert r.returncode == 0, r.stderr[-2000:]
         with open(os.path.join(d, "LOG.txt")) as f:
             ours, refills, stages = parse_log(f.read())
@@ -96,6 +105,7 @@ def main():
            "p90_us": sorted(ours)[9 * len(ours) // 10] * 1e6 if ours else None,
            "refill_convert_median_us": statistics.median(refills) * 1e6 if refills else None,
            "stage_median_us": {k: statistics.median(v) * 1e6 for k, v in stages.items() if v},
+           "compat_call_median_us": {k: [len(v), statistics.median(v)] for k, v in calls.items()} if args.trace else None,
            # parse_log over the reference's committed LOG.txt (9 430 frame iterations; its
            # authors' machine, FFTW on the CPU), evaluated in the build container
            "reference_LOG_txt_median_us": 238.42,
