@@ -57,6 +57,13 @@ __device__ __forceinline__ double sub_rn(double a, double b)
     return a - b;
 }
 
+// Complex product with the fused form spelled out (no choice left to the
+// compiler's contraction: two instantiations of one kernel round alike).
+__device__ __forceinline__ double2 cmul_fma(double2 a, double2 b)
+{
+    return make_double2(__builtin_fma(a.x, b.x, -mul_rn(a.y, b.y)), __builtin_fma(a.x, b.y, mul_rn(a.y, b.x)));
+}
+
 // Complex product with the exact rounding of g++'s inline _Complex multiply
 // on x86-64 (no FMA): used where the reference's own arithmetic is mirrored.
 __device__ __forceinline__ double2 cmul_exact(double2 a, double2 b)

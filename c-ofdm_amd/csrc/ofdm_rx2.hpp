@@ -36,13 +36,26 @@ struct Rx2Lds {
     double* red;    // phys
 };
 
+// The fused decode's per-frame table (LDS, written by sync_frame): per
+// message symbol s, RT_PER_SYM phasors {e^{i(A+Bj)}, j < 8; e^{i8B}, e^{i16B},
+// e^{i32B}; e^{iBT}}, then the channel line's two 128-carrier steps {e^{i128b},
+// e^{i(128b-K)}} (K = bD/2 + b*half: the upper half's offset), then {b, aa}.
+// A lane's ramp start e^{i(A + B lq)} is entry lq % 8 times the powers of
+// e^{i8B} the bits of lq / 8 select: one table read and three products, not a
+// sincos per lane and symbol. (Uncontracted products here: the int16 and
+// f64 instantiations must round alike, so no FMA choice is left to the
+// compiler.)
+constexpr int RT_PER_SYM = 12;
+__host__ __device__ constexpr int rt_size(int S) { return RT_PER_SYM * S + 3; }  // double2 entries
+
 // Frame f of a.starts (message body at starts[f] + start_off); corr: its S*4
-// ramp numbers {A, B, cos(B*T), sin(B*T)} (global or LDS); chan_g: nullptr,
+// ramp numbers {A, B, cos(B*T), sin(B*T)} (global or LDS), or (TAB) the
+// table above, from which the channel reciprocals are made too; chan_g: nullptr,
 // or the frame's D channel reciprocals in global memory, requested after the
 // transforms and stored to L.chl after the gains (loads issued among the
 // emit's stores would wait for them). Every thread of the 128-thread
 // workgroup calls it; it returns after a barrier (LDS reusable).
-template <bool I16>
+template <bool I16, bool TAB = false>
 __device__ __forceinline__ void rx2_frame(const RxArgs& a, long f, const Rx2Lds& L, const double* corr,
                                           const int (&pk0)[RX_DPT], int pbin, const double2* chan_g = nullptr)
 {
@@ -82,11 +95,24 @@ __device__ __forceinline__ void rx2_frame(const RxArgs& a, long f, const Rx2Lds&
             asm volatile("v_mov_b32 %0, %1" : "=v"(lq) : "v"(lane));
             // the ramp's start phasor first (its sincos temporaries die
             // before the sample registers are allocated)
-            const double* cr = corr + s * 4;
-            double sn, cs;
-            sincos(cr[0] + cr[1] * (double)lq, &sn, &cs);
-            double2 c = make_double2(cs, sn);
-            const double2 wr = make_double2(cr[2], cr[3]);
+            double2 c, wr;
+            if constexpr (TAB) {
+                const double2* rt = reinterpret_cast<const double2*>(corr) + s * RT_PER_SYM;
+                c = rt[lq & 7];
+                const int hi = lq >> 3;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const double2 p = rt[8 + k];
+                    c = cmul_exact(c, (hi >> k) & 1 ? p : make_double2(1.0, 0.0));  // x (1, 0): exact
+                }
+                wr = rt[11];
+            } else {
+                const double* cr = corr + s * 4;
+                double sn, cs;
+                sincos(cr[0] + cr[1] * (double)lq, &sn, &cs);
+                c = make_double2(cs, sn);
+                wr = make_double2(cr[2], cr[3]);
+            }
             asm volatile("" ::: "memory");
             double2 v[8];
             const long off = x0 + (long)s * Lf + lq;
@@ -106,8 +132,13 @@ __device__ __forceinline__ void rx2_frame(const RxArgs& a, long f, const Rx2Lds&
             // running product from e^{i(A + B lq)} in steps of e^{i B T}
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-                v[i] = cmul(v[i], c);
-                if (i < 7) c = cmul(c, wr);
+                if constexpr (TAB) {
+                    v[i] = cmul_fma(v[i], c);
+                    if (i < 7) c = cmul_fma(c, wr);
+                } else {
+                    v[i] = cmul(v[i], c);
+                    if (i < 7) c = cmul(c, wr);
+                }
             }
             fft_block_wave<LOGN, -1>(v, lq, L.tw, img);
             if (lq < P) L.pil[s * P + lq] = img[pbin];
@@ -120,7 +151,25 @@ __device__ __forceinline__ void rx2_frame(const RxArgs& a, long f, const Rx2Lds&
     // two named registers, not an array (an array held across the barriers
     // below went to scratch)
     double2 chv0 = make_double2(0.0, 0.0), chv1 = make_double2(0.0, 0.0);
-    if (chan_g) {  // D <= 256 = 2 x 128
+    if constexpr (TAB) {
+        // chan_char_lq's line (Frame.hpp:397-434): carrier tid's phase as the
+        // reference computes it, carrier tid + 128's by one step of the table;
+        // stored as reciprocals (conjugates of the unit phasors) for the emit
+        const double2* rt = reinterpret_cast<const double2*>(corr) + RT_PER_SYM * S;
+        const double b = rt[2].x, aa = rt[2].y;
+        const int half = D / 2;
+        double th;
+        if (tid < half)
+            th = add_rn(mul_rn(b, (double)tid), aa);
+        else
+            th = add_rn(add_rn(mul_rn(-b, (double)D) / 2, mul_rn((double)(tid - half), b)), aa);
+        double sn, cs;
+        sincos(th, &sn, &cs);
+        const double2 h = make_double2(cs, sn);
+        const double2 h2 = cmul_exact(h, tid < half && tid + 128 >= half ? rt[1] : rt[0]);
+        chv0 = make_double2(h.x, -h.y);
+        chv1 = make_double2(h2.x, -h2.y);
+    } else if (chan_g) {  // D <= 256 = 2 x 128
         chv0 = chan_g[tid < D ? tid : 0];
         chv1 = chan_g[tid + 128 < D ? tid + 128 : 0];
     }
@@ -146,7 +195,7 @@ __device__ __forceinline__ void rx2_frame(const RxArgs& a, long f, const Rx2Lds&
         const double r = 1.0 / (coef.x * coef.x + coef.y * coef.y);
         L.gain[i] = make_double2(coef.x * r / phys, -coef.y * r / phys);
     }
-    if (chan_g) {
+    if (TAB || chan_g) {
         if (tid < D) L.chl[tid] = chv0;
         if (tid + 128 < D) L.chl[tid + 128] = chv1;
     }

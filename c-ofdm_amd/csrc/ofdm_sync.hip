@@ -1202,12 +1202,12 @@ struct SyncLds {
     int* wsum;      // P + 1 window maxima
 };
 
-// One located frame's sync stage (128 threads): writes cfo_out[f], the D
-// channel reciprocals to chan and the S ramps {A, B, cos(B*T), sin(B*T)} to
-// corr (global or LDS); returns after a barrier. load_tw: fill the twiddle
+// One located frame's sync stage (128 threads): writes cfo_out[f] and the
+// frame's ramp / channel table (ofdm_rx2.hpp rt_size) to rt, in LDS over the
+// stage's small arrays; returns after a barrier. load_tw: fill the twiddle
 // tables here (else they are resident and visible).
 __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsArgs& a, long f, const SyncLds& Ls,
-                                           double2* chan, double* corr, bool load_tw)
+                                           double2* rt, bool load_tw)
 {
     // the geometry is fixed (host-checked): N = 512, cp = 128, L = 640 = 10 T
     constexpr int LOGN = 9, N = 512, T = 64, LOGM = 7, M = 128, G = 5, S5 = G * M, CP = 128, L = N + CP;
@@ -1529,19 +1529,20 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
                 if (two) cps[q + 1] = acc1;
             }
         }
-    }
-    __syncthreads();  // cfo, phi[0], phr, the LS fit and the message CP sums visible
-    const double cfo = scal[0], phr = scal[1], b = scal[2], aa = scal[3];
-    {
+        // the message symbols' CP phases, here rather than after the join:
+        // one atan2 pass on this wave instead of one on each
+        wave_lds_sync();  // cps visible
         double rs, rc;
-        sincospi(-2.0 * cfo * (double)N, &rs, &rc);
-        for (int q = 1 + tid; q < Q; q += 128) {
+        sincospi(-2.0 * scal[0] * (double)N, &rs, &rc);
+        if (t < a.S) {
+            const int q = 1 + t;
             const double2 acc = cadd(make_double2(0.0, 0.0), cps[q]);
             const double2 r = cmul_exact(acc, make_double2(rc, rs));
             phi[q] = atan2(r.y, r.x);
         }
     }
-    __syncthreads();
+    __syncthreads();  // cfo, phi[0..S], phr and the LS fit visible
+    const double cfo = scal[0], phr = scal[1], b = scal[2], aa = scal[3];
     if (tid == 0) {
         double acc = 0.0;
         for (int q = 0; q < Q; ++q) {
@@ -1549,35 +1550,31 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
             acc += phi[q];
         }
     }
-    // chan_char_lq's line, as reciprocals for the rx multiply
-    for (int i = tid; i < a.D; i += 128) {
+    __syncthreads();  // psi visible
+    // the frame's table (ofdm_rx2.hpp rt_size): one transcendental pass for
+    // every ramp and both channel steps. Message symbol s: theta(m) = A_s +
+    // B_s m over the CP-stripped body.
+    const int nt = RT_PER_SYM * a.S + 2;  // <= 128 (S <= RX_SMAX)
+    double2 val = make_double2(0.0, 0.0);
+    if (tid < nt) {
         double th;
-        if (i < half)
-            th = add_rn(mul_rn(b, (double)i), aa);
-        else
-            th = add_rn(add_rn(mul_rn(-b, (double)a.D) / 2, mul_rn((double)(i - half), b)), aa);
+        if (tid < RT_PER_SYM * a.S) {
+            const int s = tid / RT_PER_SYM, k = tid % RT_PER_SYM, q = 1 + s;
+            const double A = -2.0 * M_PI * cfo * (double)((long)q * L + a.cp) - (psi[q] * L + phi[q] * a.cp) / N - phr;
+            const double B = -2.0 * M_PI * cfo - phi[q] / N;
+            th = k < 8 ? add_rn(A, mul_rn(B, (double)k)) : mul_rn(B, k < 11 ? (double)(8 << (k - 8)) : (double)T);
+        } else {
+            const double step = mul_rn(128.0, b);
+            th = tid == RT_PER_SYM * a.S ? step : sub_rn(step, add_rn(mul_rn(b, (double)a.D) / 2, mul_rn(b, (double)half)));
+        }
         double sn, cs;
         sincos(th, &sn, &cs);
-        // the reciprocal of the unit phasor as its conjugate (|h|^2 = 1 within
-        // 2u: the product differs from the reference's per-point division by
-        // a few ulps, as the multiply by a reciprocal does anyway)
-        chan[i] = a.chan_recip ? make_double2(cs, -sn) : make_double2(cs, sn);
+        val = make_double2(cs, sn);
     }
-    __syncthreads();  // psi visible
-    // message symbols: theta(m) = A_s + B_s m over the CP-stripped body
-    for (int s = tid; s < a.S; s += 128) {
-        const int q = 1 + s;
-        const double A = -2.0 * M_PI * cfo * (double)((long)q * L + a.cp) - (psi[q] * L + phi[q] * a.cp) / N - phr;
-        const double B = -2.0 * M_PI * cfo - phi[q] / N;
-        double sn, cs;
-        sincos(B * T, &sn, &cs);
-        double* o = corr + s * 4;
-        o[0] = A;
-        o[1] = B;
-        o[2] = cs;
-        o[3] = sn;
-    }
-    __syncthreads();  // the outputs visible (LDS); the stage's LDS is free
+    __syncthreads();  // phi / psi / scal read: the table is written over them
+    if (tid < nt) rt[tid] = val;
+    if (tid == 0) rt[nt] = make_double2(b, aa);
+    __syncthreads();  // the table visible; the stage's other LDS is free
 }
 
 // ========================================================================
@@ -1605,8 +1602,8 @@ __global__ void __launch_bounds__(128, 4) stream_decode_kernel(CfoArgs c, Stream
     double2* tw9 = smem;
     double2* A = tw9 + TwLds<9>::SIZE;        // 1024: sync transforms (+ tw7) / dat / ph, then the rx images
     double2* tw7 = A + 640;                   // over A, past the CFO transforms (dead with them)
-    double* corr = reinterpret_cast<double*>(A + 1024);  // S*4 ramps
-    double2* U = reinterpret_cast<double2*>(corr + 4 * S);  // the stages' small arrays, over each other
+    double2* U = A + 1024;                    // the stages' small arrays, over each other
+    double2* rt = U + S * P;                  // the ramp / channel table: sync -> rx (rx's gains come after it)
     SyncLds Ls;
     Ls.tw9 = tw9;
     Ls.tw7 = tw7;
@@ -1627,7 +1624,7 @@ __global__ void __launch_bounds__(128, 4) stream_decode_kernel(CfoArgs c, Stream
     Lr.pil = U;
     Lr.gain = U + S * P;
     Lr.chl = A + ((S * D + 15) >> 4);  // over the images, past the decisions (rx2_frame stages it)
-    Lr.red = reinterpret_cast<double*>(Lr.gain + S * P);
+    Lr.red = reinterpret_cast<double*>(rt + std::max(S * P, rt_size(S)));
     const int lane0 = threadIdx.x & 63;
     const long f = blockIdx.x;
     if (a.count && f >= *a.count) return;  // uniform: past the speculative frame count
@@ -1637,14 +1634,13 @@ __global__ void __launch_bounds__(128, 4) stream_decode_kernel(CfoArgs c, Stream
 #pragma unroll
     for (int i = 0; i < RX_DPT; ++i) pk[i] = r.tab.rx_pack[lane0 + 64 * i];
     const int pbin = r.tab.pilot_swz[lane0];
-    double2* chan = a.chan_out + f * D;
     // the sync stage's dependent chains issue ahead of the transform-heavy
     // rx stage of the CU's other frames (priority 1 vs 0: 498 -> 478 us;
     // 2 and 3 gain less)
     __builtin_amdgcn_s_setprio(1);
-    sync_frame(c, a, f, Ls, chan, corr, true);
+    sync_frame(c, a, f, Ls, rt, true);
     __builtin_amdgcn_s_setprio(0);
-    rx2_frame<I16>(r, f, Lr, corr, pk, pbin, chan);
+    rx2_frame<I16, true>(r, f, Lr, reinterpret_cast<const double*>(rt), pk, pbin);
 }
 
 static bool stream_sync_geometry(const CfoArgs& c, const StreamParamsArgs& a, int logn, int logm, int g)
@@ -1657,9 +1653,9 @@ static bool stream_sync_geometry(const CfoArgs& c, const StreamParamsArgs& a, in
 template <bool I16>
 static hipError_t decode_launch(const CfoArgs& c, const StreamParamsArgs& a, const RxArgs& r, hipStream_t st)
 {
-    const size_t shm = sizeof(double2) * (TwLds<9>::SIZE + 1024) + sizeof(double) * 4 * a.S +
-                       std::max(sizeof(double2) * (2 * (size_t)a.S * a.P) + sizeof(double) * 2,
-                                sizeof(double2) * (a.P + 32 + 1 + a.S) + sizeof(double) * 132 + sizeof(int) * (a.P + 2));
+    const size_t rx_u = sizeof(double2) * ((size_t)a.S * a.P + std::max(a.S * a.P, rt_size(a.S))) + sizeof(double) * 2;
+    const size_t sync_u = sizeof(double2) * (a.P + 32 + 1 + a.S) + sizeof(double) * 132 + sizeof(int) * (a.P + 2);
+    const size_t shm = sizeof(double2) * (TwLds<9>::SIZE + 1024) + std::max(rx_u, sync_u);
     lds_opt_in((const void*)stream_decode_kernel<I16>, 160 * 1024);
     hipLaunchKernelGGL(stream_decode_kernel<I16>, dim3((unsigned)a.nframes), dim3(128), shm, st, c, a, r);
     return hipGetLastError();
