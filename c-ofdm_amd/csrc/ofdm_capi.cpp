@@ -152,7 +152,11 @@ struct ofdm_ctx {
         size_t bytes = 0;
     };
     Grow s_walk, s_batch, s_chan, s_pbs;
-    Grow s_pre, s_pre_done;  // find_preamble: split magnitudes, per-start counters (zero between launches)
+    // find_preamble's split form: magnitudes and per-start counters (zero
+    // between launches) for up to PRE_SCRATCH_STARTS start indices per call
+    static constexpr size_t PRE_SCRATCH_STARTS = 64;
+    double* d_pre_hv = nullptr;
+    unsigned* d_pre_done = nullptr;
     // pinned host staging for the walk records and the frame list (pageable
     // copies go through a driver bounce buffer and synchronise twice)
     Grow h_walk, h_frames;
@@ -313,10 +317,10 @@ int ofdm_destroy(ofdm_ctx* c)
                     c->d_pilot_swz, c->d_tx_code, c->d_const,
                     c->d_const_bpsk, c->d_header, c->d_preamble, c->d_templ, c->d_tspec, c->d_twm, c->d_modpre,
                     c->d_t2mask,
-                    c->d_t2tw, c->d_first, c->d_scratch, c->d_cfo_scratch};
+                    c->d_t2tw, c->d_first, c->d_scratch, c->d_cfo_scratch, c->d_pre_hv, c->d_pre_done};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
-    for (auto* g : {&c->s_walk, &c->s_batch, &c->s_chan, &c->s_pbs, &c->s_pre, &c->s_pre_done})
+    for (auto* g : {&c->s_walk, &c->s_batch, &c->s_chan, &c->s_pbs})
         if (g->p) (void)hipFree(g->p);
     for (auto* g : {&c->h_walk, &c->h_frames})
         if (g->p) (void)hipHostFree(g->p);
@@ -576,6 +580,17 @@ int ofdm_create(const ofdm_params* params, int device, ofdm_ctx** out)
     if ((rc = upload(&c->d_first, std::vector<int>{INT_MAX, 0, 0, 0}))) {
         ofdm_destroy(c);
         return rc;
+    }
+    // find_preamble's split scratch for up to PRE_SCRATCH_STARTS start indices
+    // (counters zero between launches); more starts per call take the
+    // one-workgroup form, so the entry point never allocates
+    {
+        const size_t cyc = 2 * (size_t)c->p.t2sin_size + (size_t)c->p.pr_sin_len;
+        if ((rc = upload(&c->d_pre_hv, std::vector<double>(ofdm_ctx::PRE_SCRATCH_STARTS * cyc, 0.0))) ||
+            (rc = upload(&c->d_pre_done, std::vector<unsigned>(ofdm_ctx::PRE_SCRATCH_STARTS, 0u)))) {
+            ofdm_destroy(c);
+            return rc;
+        }
     }
     if (c->t2 >= 64 && c->t2 <= 4096 && ilog2_exact(c->t2) > 0) {
         c->t2_logn = ilog2_exact(c->t2);
@@ -1075,19 +1090,13 @@ int ofdm_t2_scan(ofdm_ctx* c, const double* iq, size_t n, long start, double* re
     return OFDM_OK;
 }
 
-// Scratch of a find_preamble launch over nstarts start indices.
-static int preamble_scratch(ofdm_ctx* c, size_t nstarts, ofdm::PreambleArgs& a)
+// find_preamble's split scratch when the call fits it (else the
+// one-workgroup form: hv_scratch stays null).
+static void preamble_scratch(ofdm_ctx* c, size_t nstarts, ofdm::PreambleArgs& a)
 {
-    if (ofdm::preamble_splits(a.cycles) <= 1) return OFDM_OK;
-    int rc;
-    if ((rc = grow(c, c->s_pre, nstarts * a.cycles * sizeof(double)))) return rc;
-    if (nstarts * sizeof(unsigned) > c->s_pre_done.bytes) {
-        if ((rc = grow(c, c->s_pre_done, nstarts * sizeof(unsigned)))) return rc;
-        HIP_TRY(hipMemset(c->s_pre_done.p, 0, c->s_pre_done.bytes));
-    }
-    a.hv_scratch = static_cast<double*>(c->s_pre.p);
-    a.done = static_cast<unsigned*>(c->s_pre_done.p);
-    return OFDM_OK;
+    if (nstarts > ofdm_ctx::PRE_SCRATCH_STARTS) return;
+    a.hv_scratch = c->d_pre_hv;
+    a.done = c->d_pre_done;
 }
 
 int ofdm_find_preamble(ofdm_ctx* c, const double* iq, size_t n, const int* starts, size_t nstarts, int* idx_out,
@@ -1105,7 +1114,7 @@ int ofdm_find_preamble(ofdm_ctx* c, const double* iq, size_t n, const int* start
     a.L = (int)c->p.pr_sin_len;
     a.cycles = (int)(2 * c->p.t2sin_size + c->p.pr_sin_len);
     a.level = (double)c->p.pr_level / 1000;
-    if (int rc = preamble_scratch(c, nstarts, a)) return rc;
+    preamble_scratch(c, nstarts, a);
     hipError_t e = ofdm::launch_find_preamble(a, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "find_preamble launch");
     return OFDM_OK;
@@ -1130,7 +1139,7 @@ int ofdm_preamble_corr(ofdm_ctx* c, const double* iq, size_t n, long start, doub
     a.cycles = (int)(2 * c->p.t2sin_size + c->p.pr_sin_len);
     a.level = (double)c->p.pr_level / 1000;
     a.cor_out = cor_out;
-    if (int rc = preamble_scratch(c, 1, a)) return rc;
+    preamble_scratch(c, 1, a);
     hipError_t e = ofdm::launch_find_preamble(a, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "preamble_corr launch");
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));  // the start word is host-staged

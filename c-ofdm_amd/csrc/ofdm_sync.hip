@@ -305,7 +305,8 @@ __global__ void __launch_bounds__(PRE_THREADS) find_preamble_kernel(PreambleArgs
     const int L = a.L, C = a.cycles, n = C + L;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const long s = a.starts[blockIdx.y];
-    const int nsplit = gridDim.x, lag0 = blockIdx.x * PRE_THREADS, cnt = min(PRE_THREADS, C - lag0);
+    const int nsplit = gridDim.x, lag0 = blockIdx.x * PRE_THREADS;
+    const int cnt = nsplit == 1 ? C : min(PRE_THREADS, C - lag0);  // this workgroup's lags
     int& last_block = *reinterpret_cast<int*>(smem);  // (dynamic LDS only: the opt-in takes all 160 KB)
     double* hv = reinterpret_cast<double*>(smem + 1);  // C correlation magnitudes
     {
@@ -316,23 +317,23 @@ __global__ void __launch_bounds__(PRE_THREADS) find_preamble_kernel(PreambleArgs
         }
         __syncthreads();
         // correlation per lag, j = 0..L-1 in order (Frame.cpp:360-363), and its magnitude
-        if (t < cnt) {
+        for (int i = t; i < cnt; i += PRE_THREADS) {
             double2 e = make_double2(0.0, 0.0);
             int j = 0;
             for (; j + 8 <= L; j += 8) {  // operands a batch ahead: the chain waits on its adds alone
                 double2 xv[8], cv[8];
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
-                    xv[k] = xs[t + j + k];
+                    xv[k] = xs[i + j + k];
                     cv[k] = a.templ[j + k];
                 }
 #pragma unroll
                 for (int k = 0; k < 8; ++k) e = cadd_rn(e, cmul_exact(xv[k], cv[k]));
             }
-            for (; j < L; ++j) e = cadd_rn(e, cmul_exact(xs[t + j], a.templ[j]));
+            for (; j < L; ++j) e = cadd_rn(e, cmul_exact(xs[i + j], a.templ[j]));
             const double h = hypot(e.x, e.y);
-            hv[lag0 + t] = h;
-            if (nsplit > 1) a.hv_scratch[blockIdx.y * (long)C + lag0 + t] = h;
+            hv[lag0 + i] = h;
+            if (nsplit > 1) a.hv_scratch[blockIdx.y * (long)C + lag0 + i] = h;
         }
         if (nsplit > 1) {
             __threadfence();  // release this slice
@@ -494,11 +495,12 @@ __global__ void __launch_bounds__(PRE_THREADS) find_preamble_kernel(PreambleArgs
 hipError_t launch_find_preamble(const PreambleArgs& a, hipStream_t st)
 {
     if (a.nstarts <= 0) return hipSuccess;
-    const int nsplit = preamble_splits(a.cycles);
-    if (nsplit > 1 && (!a.hv_scratch || !a.done)) return hipErrorInvalidValue;
+    // split over workgroups when the caller provides the scratch, else one
+    // workgroup per start index
+    const int nsplit = a.hv_scratch && a.done ? preamble_splits(a.cycles) : 1;
     if (a.nstarts > 65535) return hipErrorInvalidValue;
     const size_t C = (size_t)a.cycles, nn = C + a.L;
-    const size_t corr = sizeof(double) * C + sizeof(double2) * (std::min<size_t>(C, PRE_THREADS) + a.L);
+    const size_t corr = sizeof(double) * C + sizeof(double2) * ((nsplit > 1 ? std::min<size_t>(C, PRE_THREADS) : C) + a.L);
     const size_t tail = sizeof(double) * (C + nn + nn + 1 + C + PRE_BATCH + PRE_THREADS / 64) + sizeof(int) * 2 +
                         sizeof(unsigned) * ((C + 31) / 32) + 64;
     const size_t shm = sizeof(double2) + std::max(corr, tail);

@@ -30,8 +30,8 @@ struct PreambleArgs {
     int cycles;             // 2*T2sin_size + pr_sin_len
     double level;           // pr_level / 1000
     double* cor_out;        // nullable: find_corr values, cycles per start
-    double* hv_scratch;     // nstarts * cycles (when preamble_splits(cycles) > 1)
-    unsigned* done;         // nstarts counters, zero between launches (idem)
+    double* hv_scratch;     // nullable: nstarts * cycles (the split form), else one workgroup per start
+    unsigned* done;         // nstarts counters, zero between launches (with hv_scratch)
 };
 
 struct CfoArgs {

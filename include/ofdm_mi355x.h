@@ -19,6 +19,14 @@
  *     they can be captured into a hipGraph.
  *   - One ofdm_ctx per thread (or per GPU); a ctx is not re-entrant, matching
  *     the reference (one FRAME_FORM per thread).
+ *   - Streams: rx launches keep their frame-queue counter per HIP stream, so
+ *     one ctx may run rx / fft_read on several streams at once. The detector
+ *     entry points (find_t2sin, find_preamble) and the stream receiver keep
+ *     one scratch per ctx: a ctx has at most one of those calls in flight at
+ *     a time (consecutive calls on one stream are always fine); overlapping
+ *     them on two streams takes two contexts, as INTEGRATION.md's
+ *     double-buffered receiver does. A stream call waits (on the device) for
+ *     the previous stream call's decode when it is issued on another stream.
  */
 #ifndef OFDM_MI355X_H
 #define OFDM_MI355X_H

@@ -64,6 +64,26 @@ def test_find_preamble_matches_reference_indices():
     assert got[0] + 1 == GD["preamble_begin"][0]
 
 
+def test_find_preamble_many_starts_one_workgroup_form():
+    """More start indices than the context's split scratch holds (64): each
+    start runs in one workgroup; the answers equal the split form's and the
+    reference's."""
+    m = modem(G)
+    x = GD["data"]
+    pb = int(GD["preamble_begin"][0]) - 1
+    rng = np.random.default_rng(5)
+    starts = np.concatenate([[pb - 300, pb - 1, pb, pb + 1, 10752, 19000],
+                             rng.integers(0, len(x) - 1, 94)]).astype(np.int32)
+    out = torch.zeros((len(starts),), dtype=torch.int32, device="cuda")
+    m.find_preamble(dev(x), len(x), dev(starts), len(starts), out)
+    got = host(out)
+    want = [O.find_preamble(G, x, int(s)) for s in starts]
+    assert list(got) == want
+    split = torch.zeros((8,), dtype=torch.int32, device="cuda")
+    m.find_preamble(dev(x), len(x), dev(starts[:8]), 8, split)
+    assert list(host(split)) == want[:8]
+
+
 def _golden_mwp():
     pr = GD["preamble_begin"][0]
     return GD["data"][pr: pr + GEO["preamble_len"] + GEO["message_len"]].copy()
