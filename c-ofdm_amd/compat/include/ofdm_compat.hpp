@@ -129,12 +129,24 @@ struct Chain {
     double cfo = 0.0;
     // the states after freq_shift / cp / phase (pinned), results, events
     char* hstate[3] = {};
-    char *dchan = nullptr, *hchan = nullptr, *dcons = nullptr, *hcons = nullptr;
+    char *dchan = nullptr, *hchan = nullptr, *hcons = nullptr;  // hcons: the message transform (FFT_FORM::read)
     double *dcfo = nullptr, *hcfo = nullptr;
-    void* ev[6] = {};  // cfo, state 0..2, chan, cons
+    // Modulation::demod of the channel-divided message (rx.cpp:211-220): the
+    // points and their decisions, written by the rx kernel to pinned memory
+    char* hcons_eq = nullptr;
+    uint8_t* hbits = nullptr;
+    size_t bits_bytes = 0;
+    int bits_k = 0;    // the message's bits per point
+    bool demod_armed = false;  // fft() was served: the next demod may be
+    void* ev[7] = {};  // cfo, state 0..2, chan, cons, demod
     ~Chain();
     bool alloc(Engine& e);
 };
+
+// The chain whose speculated demod the calling thread's next
+// Modulation::demod may take (set when OFDM_FORM::fft is served), or nullptr.
+void arm_demod(Chain* c);
+Chain* armed_demod();
 
 // A FRAME_FORM's mirrors and run-ahead chain (registered while alive).
 struct FrameMirrors {

@@ -331,6 +331,8 @@ complex_vector OFDM_FORM::fft()
             check(ofdm_event_synchronize(ctx_->engine().ctx, ch->ev[5]), "ofdm_event_synchronize");
             std::memcpy(fft_task.restored_buf.data(), ch->hcons, ch->cons_bytes);
             ch->fft_served = true;
+            ch->demod_armed = true;
+            ofdm_compat::arm_demod(ch);
             if (ch->chan_served) ch->stage = 0;
             return fft_task.restored_buf;
         }
@@ -422,18 +424,22 @@ double OFDM_FORM::pilot_freq_sinh()
               "ofdm_chan_estimate");
         e.d2h_pinned(ch->hchan, ch->dchan, ch->chan_bytes);
         check(ofdm_event_record(e.ctx, ch->ev[4], st), "ofdm_event_record");
+        // the message transform (OFDM_FORM::fft) and rx.cpp:214-220 behind
+        // it, the points divided by this channel (the host loop's complex
+        // division) with Modulation::demod's decisions: one rx launch writing
+        // all three straight into pinned memory
         const size_t nm = (ch->region_bytes - ch->pre_bytes) / CD;
-        check(ofdm_rx_demod(ch->msg_ctx->ctx, (const double*)(dr + ch->pre_bytes), 1, nm, nullptr, 0,
-                            (double*)ch->dcons, nullptr, nullptr, nullptr, st),
-              "ofdm_rx_demod");
-        e.d2h_pinned(ch->hcons, ch->dcons, ch->cons_bytes);
+        check(ofdm_rx_demod_read(ch->msg_ctx->ctx, (const double*)(dr + ch->pre_bytes), 1, nm,
+                                 (const double*)ch->dchan, 0, (double*)ch->hcons, (double*)ch->hcons_eq, ch->hbits, st),
+              "ofdm_rx_demod_read");
         check(ofdm_event_record(e.ctx, ch->ev[5], st), "ofdm_event_record");
+        check(ofdm_event_record(e.ctx, ch->ev[6], st), "ofdm_event_record");
         check(ofdm_event_synchronize(e.ctx, ch->ev[0]), "ofdm_event_synchronize");
         const double shift = *ch->hcfo;
         ch->cfo = shift;
         ch->stage = 1;
         ch->gen = ofdm_compat::mirror_gen(ch->region, ch->region_bytes);
-        ch->chan_served = ch->fft_served = false;
+        ch->chan_served = ch->fft_served = ch->demod_armed = false;
         return shift;
     }
     const DevRange x = stage_in(*ctx_, 1, output[0], (size_t)size * CD);

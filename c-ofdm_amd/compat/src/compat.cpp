@@ -6,6 +6,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cctype>
 #include <cstdlib>
 #include <cstring>
@@ -323,16 +324,24 @@ bool mirror_clean(const void* p, size_t n, size_t gen)
     return lo == hi;
 }
 
+namespace {
+thread_local Chain* t_demod = nullptr;
+}
+
+void arm_demod(Chain* c) { t_demod = c; }
+Chain* armed_demod() { return t_demod; }
+
 Chain::~Chain()
 {
+    if (t_demod == this) t_demod = nullptr;
     if (!mwp_ctx) return;
     ofdm_ctx* c = mwp_ctx->ctx;
     for (int i = 0; i < 3; ++i) {
         if (hstate[i]) ofdm_host_free(c, hstate[i]);
     }
-    for (void* d : {(void*)dchan, (void*)dcons, (void*)dcfo})
+    for (void* d : {(void*)dchan, (void*)dcfo})
         if (d) ofdm_device_free(c, d);
-    for (void* h : {(void*)hchan, (void*)hcons, (void*)hcfo})
+    for (void* h : {(void*)hchan, (void*)hcons, (void*)hcfo, (void*)hcons_eq, (void*)hbits})
         if (h) ofdm_host_free(c, h);
     for (void* e : ev)
         if (e) ofdm_event_destroy(c, e);
@@ -353,12 +362,16 @@ bool Chain::alloc(Engine& e)
     dchan = static_cast<char*>(p);
     check(ofdm_host_alloc(c, chan_bytes, &p), "ofdm_host_alloc");
     hchan = static_cast<char*>(p);
-    check(ofdm_device_alloc(c, cons_bytes, &p), "ofdm_device_alloc");
-    dcons = static_cast<char*>(p);
     check(ofdm_host_alloc(c, cons_bytes, &p), "ofdm_host_alloc");
     hcons = static_cast<char*>(p);
     check(ofdm_host_alloc(c, sizeof(double), &p), "ofdm_host_alloc");
     hcfo = static_cast<double*>(p);
+    check(ofdm_host_alloc(c, cons_bytes, &p), "ofdm_host_alloc");
+    hcons_eq = static_cast<char*>(p);
+    bits_bytes = (size_t)msg_ctx->geo.bytes_per_frame;
+    bits_k = msg_ctx->params.mod_type;
+    check(ofdm_host_alloc(c, bits_bytes, &p), "ofdm_host_alloc");
+    hbits = static_cast<uint8_t*>(p);
     for (auto& v : ev) check(ofdm_event_create(c, &v), "ofdm_event_create");
     check(ofdm_device_alloc(c, sizeof(double), &p), "ofdm_device_alloc");
     dcfo = static_cast<double*>(p);
@@ -463,6 +476,24 @@ std::vector<uint8_t> Modulation::demod(complex_vector& in)
     const size_t n = in.size(), nb = (n * mod_index + 7) / 8;
     std::vector<uint8_t> out(nb);
     if (!n) return out;
+    // rx.cpp:214-220 run ahead by the frame's chain: served when these are
+    // exactly the points it divided and decided (same kernels, same inputs)
+    if (ofdm_compat::Chain* ch = ofdm_compat::armed_demod()) {
+        ofdm_compat::arm_demod(nullptr);
+        if (ch->demod_armed && (int)mod_index == ch->bits_k && n * sizeof(complex_double) == ch->cons_bytes &&
+            nb == ch->bits_bytes) {
+            ch->demod_armed = false;
+            check(ofdm_event_synchronize(ctx_->engine().ctx, ch->ev[6]), "ofdm_event_synchronize");
+            if (std::memcmp(in.data(), ch->hcons_eq, ch->cons_bytes) == 0) {
+                std::memcpy(out.data(), ch->hbits, nb);
+                if (modulation != bpsk)  // clamped in place (modulation.cpp:70-75)
+                    for (auto& z : in)
+                        z = complex_double(std::fmin(std::fmax(z.real(), -1.0), 1.0),
+                                           std::fmin(std::fmax(z.imag(), -1.0), 1.0));
+                return out;
+            }
+        }
+    }
     void* dp = ctx_->buf(0, n * sizeof(complex_double));
     void* db = ctx_->buf(1, nb);
     ctx_->h2d(dp, in.data(), n * sizeof(complex_double));

@@ -895,7 +895,8 @@ int ofdm_tx_frames(ofdm_ctx* c, const uint8_t* bytes, size_t nframes, double* fr
 // ofdm_rx_demod / ofdm_rx_demod_i16: exactly one of iq, iq16 is set.
 static int rx_demod_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, size_t nframes, size_t frame_stride,
                          const double* chan, size_t chan_stride, double* constell_out, uint8_t* bytes_out,
-                         const uint8_t* ref_bytes, unsigned long long* bit_errors, void* stream)
+                         const uint8_t* ref_bytes, unsigned long long* bit_errors, void* stream,
+                         double* read_out = nullptr)
 {
     if (!c || (!iq && !iq16)) return fail(OFDM_ERR_INVALID, "null argument");
     if (iq16 && ((uintptr_t)iq16 & 3)) return fail(OFDM_ERR_INVALID, "iq16 must be 4-byte aligned");
@@ -915,6 +916,7 @@ static int rx_demod_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, siz
     a.chan = reinterpret_cast<const double2*>(chan);
     a.chan_stride = (long)chan_stride;
     a.constell = reinterpret_cast<double2*>(constell_out);
+    a.read_out = reinterpret_cast<double2*>(read_out);
     a.bytes = bytes_out;
     a.ref = ref_bytes;
     a.bit_errors = bit_errors;
@@ -972,6 +974,15 @@ int ofdm_rx_demod_i16(ofdm_ctx* c, const int16_t* iq16, size_t nframes, size_t f
     if (!iq16) return fail(OFDM_ERR_INVALID, "null argument");
     return rx_demod_impl(c, nullptr, iq16, nframes, frame_stride, chan, chan_stride, constell_out, bytes_out,
                          ref_bytes, bit_errors, stream);
+}
+
+int ofdm_rx_demod_read(ofdm_ctx* c, const double* iq, size_t nframes, size_t frame_stride, const double* chan,
+                       size_t chan_stride, double* read_out, double* constell_out, uint8_t* bytes_out, void* stream)
+{
+    if (!iq || !chan || !read_out) return fail(OFDM_ERR_INVALID, "null argument");
+    if (!aligned16(read_out)) return fail(OFDM_ERR_INVALID, "complex buffers must be 16-byte aligned");
+    return rx_demod_impl(c, iq, nullptr, nframes, frame_stride, chan, chan_stride, constell_out, bytes_out, nullptr,
+                         nullptr, stream, read_out);
 }
 
 int ofdm_demap(ofdm_ctx* c, double* points, size_t n, uint8_t* bytes_out, void* stream)

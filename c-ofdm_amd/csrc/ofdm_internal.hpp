@@ -51,6 +51,7 @@ struct RxArgs {
     long chan_stride;           // complex elements between frames (0 = shared)
     bool chan_recip;            // chan holds the divisors' reciprocals (multiply instead of divide)
     double2* constell;          // nullable
+    double2* read_out;          // nullable (with chan): FFT_FORM::read's points, before the channel divisor
     uint8_t* bytes;             // nullable
     const uint8_t* ref;         // nullable
     unsigned long long* bit_errors;  // nullable

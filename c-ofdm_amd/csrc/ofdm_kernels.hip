@@ -711,6 +711,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
             int d = t + T * i, gi = s * P + (pk[i] >> 16);
             asm volatile("" : "+v"(d), "+v"(gi));
             double2 o = cmul_exact(yv, gain[gi]);
+            if (a.read_out) store_nt(a.read_out + (f * S + s) * D + d, o);
             const double2 cv = chan_lds ? chl[d] : load_untracked(chan + d);
             o = a.chan_recip ? cmul_exact(o, cv) : cdiv_exact(o, cv);
             if (a.constell) store_nt(a.constell + (f * S + s) * D + d, o);

@@ -85,6 +85,7 @@ SIGNATURES = {
     "ofdm_memcpy_h2d": (_I, [_V, _V, _V, _SZ, _V]),
     "ofdm_memcpy_d2h": (_I, [_V, _V, _V, _SZ, _V]),
     "ofdm_copy": (_I, [_V, _V, _V, _SZ, _V]),
+    "ofdm_rx_demod_read": (_I, [_V, _V, _SZ, _SZ, _V, _SZ, _V, _V, _V, _V]),
     "ofdm_memset_device": (_I, [_V, _V, _I, _SZ, _V]),
     "ofdm_stream_synchronize": (_I, [_V, _V]),
     "ofdm_tx_modulate": (_I, [_V, _V, _SZ, _V, _SZ, _V, C.POINTER(Channel), _V]),

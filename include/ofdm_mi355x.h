@@ -205,6 +205,16 @@ int ofdm_rx_demod_i16(ofdm_ctx* ctx, const int16_t* iq16, size_t nframes, size_t
                       const uint8_t* ref_bytes, unsigned long long* bit_errors,
                       void* stream);
 
+/* ofdm_rx_demod with a channel divisor that also writes FFT_FORM::read's
+ * points before the division (read_out, npts per frame): one launch for
+ * rx.cpp:211-220 (message.fft(), the host loop dividing by chan_char_lq(),
+ * Modulation::demod). read_out and constell_out may be page-locked host
+ * memory from ofdm_host_alloc (the kernel writes it directly). */
+int ofdm_rx_demod_read(ofdm_ctx* ctx, const double* iq, size_t nframes, size_t frame_stride,
+                       const double* chan, size_t chan_stride,
+                       double* read_out, double* constell_out, uint8_t* bytes_out,
+                       void* stream);
+
 /* Modulation::demod alone on n points (modulation.cpp:53-87): clamps `points`
  * IN PLACE for QAM (as the reference does) and writes n*k/8 bytes (rounded up,
  * last byte left-aligned as bit_stream_converter pads). Device pointers. */

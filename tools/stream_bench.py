@@ -28,6 +28,8 @@ import oracle as O  # noqa: E402  (config dicts and geometry only)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=16384)
+    ap.add_argument("--config", choices=("D", "B", "C"), default="D",
+                    help="frame geometry: D (config.txt, the fused decode), B (2048 carriers) or C (4096)")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--snr-db", type=float, default=20.0)
     ap.add_argument("--chunk", type=int, default=0)
@@ -42,7 +44,7 @@ def main():
     import torch
     import ofdm_mi355x as M
 
-    cfg = dict(O.DEFAULT)
+    cfg = dict({"D": O.DEFAULT, "B": O.CONFIG_B, "C": O.CONFIG_C}[args.config])
     g = O.geometry(cfg)
     m = M.Modem(cfg, 0)
     if args.walk_tuning:
@@ -115,8 +117,8 @@ def main():
     # located frame's constellation and payload bytes written
     esz = 4 if args.i16 else 16
     alg = n * esz + found * (16 * g["npts"] + g["bytes_per_frame"])
-    res = {"workload": "config4_stream_D_frames_gaps0-4096_cfo0.004_awgn%gdB%s"
-                       % (args.snr_db, "_int16" if args.i16 else ""),
+    res = {"workload": "config4_stream_%s_frames_gaps0-4096_cfo0.004_awgn%gdB%s"
+                       % (args.config, args.snr_db, "_int16" if args.i16 else ""),
            "stream_samples": n, "frames_sent": nf, "frames_found": found, "frames_error_free": ok,
            "ms": round(ms, 3), "G_stream_samples_per_s": round(n / ms / 1e6, 2),
            "frames_per_s": round(found / ms * 1e3), "stream_GB": round(n * esz / 1e9, 3),
