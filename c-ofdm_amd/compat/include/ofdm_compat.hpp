@@ -138,7 +138,10 @@ struct Chain {
     size_t bits_bytes = 0;
     int bits_k = 0;    // the message's bits per point
     bool demod_armed = false;  // fft() was served: the next demod may be
-    void* ev[7] = {};  // cfo, state 0..2, chan, cons, demod
+    // events: [0] the CFO landed, [3] the three states, [6] everything (a
+    // served member waits for the point its result needs; fewer records cost
+    // less host time than they could save in waiting)
+    void* ev[7] = {};
     ~Chain();
     bool alloc(Engine& e);
 };

@@ -113,7 +113,7 @@ ofdm_compat::Chain* served(const void* form, int stage, const void* p, size_t n)
 void serve_state(Context& ctx, ofdm_compat::Chain& ch, int k)
 {
     ofdm_compat::Engine& e = ctx.engine();
-    check(ofdm_event_synchronize(e.ctx, ch.ev[1 + k]), "ofdm_event_synchronize");
+    check(ofdm_event_synchronize(e.ctx, ch.ev[3]), "ofdm_event_synchronize");  // the three states
     ofdm_compat::Mirror* m = ofdm_compat::find_mirror(ch.region, ch.region_bytes);
     std::memcpy(ch.region, ch.hstate[k], ch.region_bytes);
     const size_t off = ch.region - m->host;
@@ -328,7 +328,7 @@ complex_vector OFDM_FORM::fft()
     const size_t np = (size_t)usefull_size;
     if (ofdm_compat::Chain* ch = served(this, 4, output[0], (size_t)size * CD)) {
         if (this == ch->msg_form && !ch->fft_served && np * CD == ch->cons_bytes) {
-            check(ofdm_event_synchronize(ctx_->engine().ctx, ch->ev[5]), "ofdm_event_synchronize");
+            check(ofdm_event_synchronize(ctx_->engine().ctx, ch->ev[6]), "ofdm_event_synchronize");
             std::memcpy(fft_task.restored_buf.data(), ch->hcons, ch->cons_bytes);
             ch->fft_served = true;
             ch->demod_armed = true;
@@ -412,10 +412,8 @@ double OFDM_FORM::pilot_freq_sinh()
         r.m->stale_hi = r.m->stale_lo + ch->region_bytes;
         check(ofdm_freq_shift(mw, (double*)dr, 1, nw, nw, ch->dcfo, st), "ofdm_freq_shift");
         e.d2h_pinned(ch->hstate[0], dr, ch->region_bytes);
-        check(ofdm_event_record(e.ctx, ch->ev[1], st), "ofdm_event_record");
         check(ofdm_cp_sync(mw, (double*)dr, 1, nw, nsym, st), "ofdm_cp_sync");
         e.d2h_pinned(ch->hstate[1], dr, ch->region_bytes);
-        check(ofdm_event_record(e.ctx, ch->ev[2], st), "ofdm_event_record");
         check(ofdm_phase_sync(mw, (double*)dr, 1, nw, nw, nullptr, 0, st), "ofdm_phase_sync");
         e.d2h_pinned(ch->hstate[2], dr, ch->region_bytes);
         check(ofdm_event_record(e.ctx, ch->ev[3], st), "ofdm_event_record");
@@ -423,7 +421,6 @@ double OFDM_FORM::pilot_freq_sinh()
                                  ch->chan_bytes / CD, st),
               "ofdm_chan_estimate");
         e.d2h_pinned(ch->hchan, ch->dchan, ch->chan_bytes);
-        check(ofdm_event_record(e.ctx, ch->ev[4], st), "ofdm_event_record");
         // the message transform (OFDM_FORM::fft) and rx.cpp:214-220 behind
         // it, the points divided by this channel (the host loop's complex
         // division) with Modulation::demod's decisions: one rx launch writing
@@ -432,7 +429,6 @@ double OFDM_FORM::pilot_freq_sinh()
         check(ofdm_rx_demod_read(ch->msg_ctx->ctx, (const double*)(dr + ch->pre_bytes), 1, nm,
                                  (const double*)ch->dchan, 0, (double*)ch->hcons, (double*)ch->hcons_eq, ch->hbits, st),
               "ofdm_rx_demod_read");
-        check(ofdm_event_record(e.ctx, ch->ev[5], st), "ofdm_event_record");
         check(ofdm_event_record(e.ctx, ch->ev[6], st), "ofdm_event_record");
         check(ofdm_event_synchronize(e.ctx, ch->ev[0]), "ofdm_event_synchronize");
         const double shift = *ch->hcfo;
@@ -541,7 +537,7 @@ complex_vector& PREAMBLE_FORM::chan_char_lq()
     COMPAT_TRACE("PREAMBLE_FORM::chan_char_lq");
     if (ofdm_compat::Chain* ch = served(this, 4, output[0], (size_t)size * CD)) {
         if (this == ch->pre_form && !ch->chan_served && chan_est.size() * CD == ch->chan_bytes) {
-            check(ofdm_event_synchronize(ctx_->engine().ctx, ch->ev[4]), "ofdm_event_synchronize");
+            check(ofdm_event_synchronize(ctx_->engine().ctx, ch->ev[6]), "ofdm_event_synchronize");
             std::memcpy(chan_est.data(), ch->hchan, ch->chan_bytes);
             ch->chan_served = true;
             if (ch->fft_served) ch->stage = 0;
