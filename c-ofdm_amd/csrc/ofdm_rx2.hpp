@@ -185,15 +185,15 @@ __device__ __forceinline__ void rx2_frame(const RxArgs& a, long f, const Rx2Lds&
     __syncthreads();
     const double phys = L.red[0] / ((double)(P * S) * a.pilot_ampl);
     // out = (F/phys) / ((F[s,p]/phys) / (F[0,p]/phys)) = F * gain[s][j]   (Frame.cpp:82-93)
+    // with gain = F[0,p] conj(F[s,p]) / (|F[s,p]|^2 phys): the points are
+    // multiplied, not divided as the reference does (within rounding: the
+    // constellation to ~1e-15 relative), phys cancelling inside coef
     for (int i = tid; i < S * P; i += 128) {
         const int j = i % P;
-        const double2 c0 = make_double2(L.pil[j].x / phys, L.pil[j].y / phys);
-        const double2 cs = make_double2(L.pil[i].x / phys, L.pil[i].y / phys);
-        const double2 coef = cdiv_exact(cs, c0);
-        // the divisor's reciprocal as conj / |.|^2 (the points are multiplied,
-        // not divided as the reference does: within rounding either way)
-        const double r = 1.0 / (coef.x * coef.x + coef.y * coef.y);
-        L.gain[i] = make_double2(coef.x * r / phys, -coef.y * r / phys);
+        const double2 c0 = L.pil[j], cs = L.pil[i];
+        const double2 num = cmul_exact(c0, make_double2(cs.x, -cs.y));
+        const double r = 1.0 / mul_rn(add_rn(mul_rn(cs.x, cs.x), mul_rn(cs.y, cs.y)), phys);
+        L.gain[i] = make_double2(num.x * r, num.y * r);
     }
     if (TAB || chan_g) {
         if (tid < D) L.chl[tid] = chv0;

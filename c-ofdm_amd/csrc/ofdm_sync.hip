@@ -1415,11 +1415,13 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
         const double slope0 = -2.0 * M_PI * cfo - phi[0] / N;
         double phr;
         {
-            double sn, cs, ws, wc;
+            double sn, cs;
             sincos(slope0 * (double)t, &sn, &cs);
-            sincos(slope0 * (double)T, &ws, &wc);
             double2 cc = make_double2(cs, sn);
-            const double2 wv = make_double2(wc, ws);
+            // the step e^{i slope0 T} as lane T/2's phasor squared (T = 64):
+            // a shuffle and a product instead of a second sincos pass
+            const double2 ch = make_double2(__shfl(cc.x, T / 2), __shfl(cc.y, T / 2));
+            const double2 wv = cmul_exact(ch, ch);
             double2 acc = make_double2(0.0, 0.0);
 #pragma unroll
             for (int r = 0; r < RMAX; ++r) {
@@ -1451,9 +1453,18 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
             acc = cadd(acc, make_double2(bacc.x * isn, bacc.y * isn));
             acc = block_sum2<T>(acc, red);
             phr = atan2(acc.y, acc.x);
-            double rs2, rc2;
-            sincos(-phr, &rs2, &rc2);
-            const double2 rot = make_double2(rc2, rs2);
+            // e^{-i phr} = conj(acc) / |acc| (acc is uniform: a uniform
+            // branch keeps sincos for a zero or non-finite sum)
+            double2 rot;
+            const double ha = hypot(acc.x, acc.y);
+            if (ha > 0.0 && ha <= DBL_MAX) {
+                const double ir = 1.0 / ha;
+                rot = make_double2(acc.x * ir, -acc.y * ir);
+            } else {
+                double rs2, rc2;
+                sincos(-phr, &rs2, &rc2);
+                rot = make_double2(rc2, rs2);
+            }
             if (t < a.P) pil[t] = cmul_exact(pz, rot);
 #pragma unroll
             for (int u = 0; u < 2; ++u)
@@ -1465,23 +1476,25 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
         acc = block_sum2<T>(make_double2(acc, 0.0), red).x;
         const double phys = acc / ((double)a.P * a.pilot_ampl);
         // arg((F/phys)/coef/mod_pre) (Frame.hpp:397-405 over FFT_FORM::read,
-        // Frame.cpp:82-93): only the angle is used, so the two complex
-        // divisions become products with the conjugates (same argument: a
-        // positive real factor |coef|^2 |mod_pre|^2 phys apart), for a finite
-        // positive phys; otherwise the reference's divisions verbatim
+        // Frame.cpp:82-93): only the angle is used, so for a finite positive
+        // phys it is arg(F conj(mod_pre)) (a positive real factor apart; coef
+        // is 1 to the last bit, below); otherwise the reference's divisions
+        // verbatim
         const bool plain = phys > 0.0 && phys <= DBL_MAX;  // uniform
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int i = t + T * u;
             if (i < half) {
                 const int j = dslot[u];
-                const double2 p0 = make_double2(pil[j].x / phys, pil[j].y / phys);
-                const double2 coef = cdiv_exact(p0, p0);
                 double2 q;
                 if (plain) {
-                    q = cmul_exact(cmul_exact(dat[i], make_double2(coef.x, -coef.y)),
-                                   make_double2(mpre[u].x, -mpre[u].y));
+                    // coef = (F/phys)/(F/phys) of the one preamble symbol is 1
+                    // up to its last bit (Smith's division of a number by
+                    // itself): its angle, ~1e-16, is dropped with the division
+                    q = cmul_exact(dat[i], make_double2(mpre[u].x, -mpre[u].y));
                 } else {
+                    const double2 p0 = make_double2(pil[j].x / phys, pil[j].y / phys);
+                    const double2 coef = cdiv_exact(p0, p0);
                     const double2 fs = make_double2(dat[i].x / phys, dat[i].y / phys);
                     q = cdiv_exact(cdiv_exact(fs, coef), mpre[u]);
                 }
