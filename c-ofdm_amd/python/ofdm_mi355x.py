@@ -254,6 +254,18 @@ class Modem:
                                   _ptr(constell_out), _ptr(bytes_out), _ptr(ref), _ptr(bit_errors),
                                   _stream(stream)))
 
+    def rx_read(self, iq, nframes: int, chan, read_out, frame_stride: int | None = None, chan_stride: int = 0,
+                constell_out=None, bytes_out=None, stream=None):
+        """ofdm_rx_demod_read: rx with a channel divisor that also writes
+        FFT_FORM::read's points before the division."""
+        stride = self.geo.message_len if frame_stride is None else frame_stride
+        check(lib().ofdm_rx_demod_read(self.h, _ptr(iq), nframes, stride, _ptr(chan), chan_stride, _ptr(read_out),
+                                       _ptr(constell_out), _ptr(bytes_out), _stream(stream)))
+
+    def copy(self, dst, src, nbytes: int, stream=None):
+        """ofdm_copy: a kernel copy on the stream (device or page-locked memory)."""
+        check(lib().ofdm_copy(self.h, _ptr(dst), _ptr(src), nbytes, _stream(stream)))
+
     def rx_i16(self, iq16, nframes: int, frame_stride: int | None = None, chan=None, chan_stride: int = 0,
                constell_out=None, bytes_out=None, ref=None, bit_errors=None, stream=None):
         """rx on complex<int16> wire samples (frame_stride in complex samples)."""

@@ -161,6 +161,64 @@ def test_rx_golden_capture_with_channel_estimate():
     assert np.array_equal(host(out), gd["payload"])
 
 
+def test_rx_demod_read_one_launch_equals_rx_with_and_without_channel():
+    """ofdm_rx_demod_read (the drop-in's run-ahead of rx.cpp:211-220): its
+    read_out equals rx without a divisor (FFT_FORM::read), its points and
+    bytes equal rx with the divisor, bit for bit; outputs in device memory or
+    written straight into page-locked host memory alike."""
+    cfg = CC
+    m = modem("C")
+    g = O.geometry(cfg)
+    nf, D = 3, cfg["num_data_subc"]
+    data = payload(nf * g["bytes_per_frame"], seed=21)
+    iq = dev(O.awgn(O.tx_batch(cfg, data, nf), 0.05, seed=22))
+    rng = np.random.default_rng(23)
+    chan = dev(np.exp(1j * rng.uniform(-0.3, 0.3, nf * D)) * rng.uniform(0.8, 1.2, nf * D))
+    npts = nf * g["npts"]
+    read0 = torch.zeros((npts,), dtype=torch.complex128, device="cuda")
+    m.rx(iq, nf, constell_out=read0)
+    cons1 = torch.zeros((npts,), dtype=torch.complex128, device="cuda")
+    out1 = torch.zeros((nf * g["bytes_per_frame"],), dtype=torch.uint8, device="cuda")
+    m.rx(iq, nf, chan=chan, chan_stride=D, constell_out=cons1, bytes_out=out1)
+    for pinned in (False, True):
+        kw = {"dtype": torch.complex128}
+        read = torch.zeros((npts,), **kw, pin_memory=True) if pinned else torch.zeros((npts,), **kw, device="cuda")
+        cons = torch.zeros((npts,), **kw, pin_memory=True) if pinned else torch.zeros((npts,), **kw, device="cuda")
+        out = (torch.zeros((nf * g["bytes_per_frame"],), dtype=torch.uint8, pin_memory=True) if pinned else
+               torch.zeros((nf * g["bytes_per_frame"],), dtype=torch.uint8, device="cuda"))
+        m.rx_read(iq, nf, chan, read, chan_stride=D, constell_out=cons, bytes_out=out)
+        torch.cuda.synchronize()
+        assert torch.equal(read.cpu(), read0.cpu())
+        assert torch.equal(cons.cpu(), cons1.cpu())
+        assert torch.equal(out.cpu(), out1.cpu())
+    # the division is the reference's (libgcc Smith division, main.cpp:69-71)
+    c = host(cons1).reshape(nf, -1)
+    want = host(read0).reshape(nf, -1) / np.tile(host(chan).reshape(nf, D), (1, g["npts"] // D))
+    assert rel_err(c, want) < 1e-14
+
+
+@pytest.mark.parametrize("n", [1, 15, 16, 17, 4096, 100003])
+def test_copy_kernel_device_and_pinned(n):
+    """ofdm_copy: device <-> device / page-locked host, aligned (16-B body +
+    tail) and misaligned (byte) forms."""
+    m = modem("D")
+    src = torch.randint(0, 256, (n + 64,), dtype=torch.uint8, device="cuda")
+    for off_s, off_d in ((0, 0), (16, 32), (3, 5)):
+        want = src[off_s:off_s + n].cpu()
+        d = torch.zeros((n + 64,), dtype=torch.uint8, device="cuda")
+        m.copy(d[off_d:], src[off_s:], n)
+        h = torch.zeros((n + 64,), dtype=torch.uint8, pin_memory=True)
+        m.copy(h[off_d:], src[off_s:], n)
+        back = torch.zeros((n + 64,), dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        m.copy(back[off_d:], h[off_d:], n)
+        torch.cuda.synchronize()
+        assert torch.equal(d[off_d:off_d + n].cpu(), want)
+        assert torch.equal(h[off_d:off_d + n], want)
+        assert torch.equal(back[off_d:off_d + n].cpu(), want)
+        assert int(d[:off_d].sum()) == 0 and int(d[off_d + n:].sum()) == 0  # nothing past the range
+
+
 @pytest.mark.parametrize("k", [1, 2, 4, 6, 8])
 def test_demap_and_map_match_oracle(k):
     cfg = dict(ALL_CONFIGS["D"], mod_type=k)
