@@ -447,6 +447,12 @@ def main():
         # never touches the GPU itself; rank 0 prints the JSON line
         sys.exit(ofdm_dist.launch_ranks(args.gpus, os.path.abspath(__file__), sys.argv[1:]))
 
+    # exactly one line on stdout (rank 0's JSON): every other write to fd 1,
+    # including C++ library banners (gloo's peer-connection notes), goes to
+    # stderr
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
     import torch
     import ofdm_mi355x as M
 
@@ -602,7 +608,7 @@ def main():
         torch.cuda.empty_cache()
         result["config3"] = config3_leg(args, dist, dev, world, rank, M)
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=json_out, flush=True)
     if dist:
         dist.destroy_process_group()
 
