@@ -225,16 +225,24 @@ def run_local(rxs: list[ShardedStreamRx], walks: list) -> list[int]:
 
 def torch_exchange(dist, device):
     """all-gather of one int64 row per rank over the job's process group (RCCL
-    over xGMI with the rows on the GPU, gloo on the host)."""
+    over xGMI with the rows on the GPU, gloo on the host). On the GPU the
+    rows travel on a side stream of their own: an RCCL collective waits for
+    the issuing stream's pending work, and on the receiver's stream that is
+    the speculative decode of this very call, which the exchange should run
+    beside, not after."""
+    import contextlib
+
     import torch
+    side = torch.cuda.Stream(device) if device.type == "cuda" else None
 
     def exchange(row):
-        t = torch.from_numpy(np.ascontiguousarray(row)).to(device)
         if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
             return [row]
-        out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
-        dist.all_gather(out, t)
-        return [o.cpu().numpy() for o in out]
+        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            t = torch.from_numpy(np.ascontiguousarray(row)).to(device)
+            out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+            dist.all_gather(out, t)
+            return [o.cpu().numpy() for o in out]
     return exchange
 
 
