@@ -24,17 +24,19 @@ def main():
             calls.append({"i16": "<true>" in c["Kernel_Name"], "walk_us": (t[0][1] - t[0][0]) / 1e3,
                           "compact_us": (t[1][1] - t[1][0]) / 1e3, "decode_us": (t[2][1] - t[2][0]) / 1e3,
                           "gap1_us": (t[1][0] - t[0][1]) / 1e3, "gap2_us": (t[2][0] - t[1][1]) / 1e3,
-                          "span_us": (t[2][1] - t[0][0]) / 1e3})
+                          "span_us": (t[2][1] - t[0][0]) / 1e3, "walk_start": t[0][0], "decode_end": t[2][1]})
+    for c0, c1 in zip(calls, calls[1:]):  # decode end -> next call's walk start (host between calls)
+        c0["gap_next_us"] = (c1["walk_start"] - c0["decode_end"]) / 1e3
     out = {"source": path, "note": "trace of bench.py --stream-pipeline 1 (serial calls); mean over each "
                                    "leg's last n calls"}
     for leg, i16 in (("f64", False), ("int16", True)):
         cs = [c for c in calls if c["i16"] == i16 and c["gap1_us"] >= 0 and c["gap2_us"] >= 0]
-        cs = cs[-n:]
+        cs = [c for c in cs if "gap_next_us" in c and 0 <= c["gap_next_us"] < 5000][-n:]
         if not cs:
             continue
         m = lambda k: round(sum(c[k] for c in cs) / len(cs), 1)
         out[leg] = {"calls": len(cs), **{k: m(k) for k in ("walk_us", "compact_us", "decode_us", "gap1_us",
-                                                          "gap2_us", "span_us")},
+                                                          "gap2_us", "span_us", "gap_next_us")},
                     "walk_plus_decode_us": round(m("walk_us") + m("decode_us"), 1)}
     print(json.dumps(out, indent=1))
 
