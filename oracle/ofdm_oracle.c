@@ -731,8 +731,10 @@ static inline uint32_t lowbias32(uint32_t x)
 }
 
 /* Counter-based Box-Muller AWGN; same definition as the HIP tx kernel
- * (ofdm_kernels.hip awgn_sample): 24-bit uniforms from a lowbias32 hash of the
- * 64-bit sample counter and seed. The GPU evaluates log/sin/cos on its FP32
+ * (ofdm_kernels.hip awgn_sample): 24-bit uniforms from a lowbias32 hash h1 of
+ * the 64-bit sample counter and seed, u1 from h1 and u2 from h1 times the
+ * 32-bit Fibonacci multiplier (the pair spans h1's 2^32 values either way;
+ * the multiply replaces a second hash). The GPU evaluates log/sin/cos on its FP32
  * units, so the two agree to ~1e-6 of noise_std, not bitwise. A channel model
  * of this repo (the reference's channel is the radio, python_code/channel.py). */
 void orc_awgn(double* xd, long n, double noise_std, unsigned long long seed,
@@ -755,7 +757,7 @@ void orc_awgn_mt(double* xd, long n, double noise_std, unsigned long long seed,
     for (long i = 0; i < n; i++) {
         uint64_t g = off + (uint64_t)i;
         uint32_t h1 = lowbias32((uint32_t)g ^ lowbias32((uint32_t)(g >> 32) ^ k1) ^ k0);
-        uint32_t h2 = lowbias32(h1 ^ 0x632BE5ABu);
+        uint32_t h2 = h1 * 0x9E3779B9u; /* Fibonacci multiplier: (u1, u2) on a rank-1 lattice */
         double u1 = (double)(float)((float)((h1 >> 8) + 1) * 0x1.0p-24f);
         double u2 = (double)(float)((float)(h2 >> 8) * 0x1.0p-24f);
         double r = sqrt(-2.0 * log(u1)) * sc;
