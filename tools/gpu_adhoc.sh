@@ -1,5 +1,5 @@
+# Scratch slot for one-off GPU commands (`gpurun -- bash tools/gpu_adhoc.sh`);
+# its content changes with the experiment at hand and is not part of any flow.
 export TMPDIR=/tmp
-R=$GRAFT_REPO_ROOT
-mkdir -p $R/gpurun_out
-cd $R
-bash tools/gpu_stream_check.sh r03o && TAG=r03o LIBS="ab/base.so product" bash tools/stream_ab.sh
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+timeout -k 10 120 python3 tools/ab_step.py
