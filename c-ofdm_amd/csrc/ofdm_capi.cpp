@@ -1725,7 +1725,7 @@ int ofdm_walk_tuning_default(ofdm_walk_tuning* o)
     if (!o) return fail(OFDM_ERR_INVALID, "null argument");
     *o = ofdm_walk_tuning{};
     o->chunks_per_slot = 1;
-    o->halo_milli = 2000;
+    o->halo_milli = 3000;
     o->ext_milli = 0;
     o->exact_search = 0;
     o->t2_f32 = 1;

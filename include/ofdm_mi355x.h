@@ -383,7 +383,7 @@ int ofdm_stream_shard_margins(const ofdm_ctx* ctx, long* halo_out, long* tail_ou
  * can make the walk differ from the reference (tests use 0 and 1). */
 typedef struct ofdm_walk_tuning {
     long chunks_per_slot; /* chunks per resident walker (>= 1; default 1)       */
-    long halo_milli;      /* walk-in halo, 1/1000 frames (default 2000)         */
+    long halo_milli;      /* walk-in halo, 1/1000 frames (default 3000)         */
     long ext_milli;       /* walk-on past the core end, 1/1000 frames (0)       */
     int exact_search;     /* 1: serial-recurrence preamble search (default 0)   */
     int t2_f32;           /* 1: certified FP32 T2 screen (default 1)            */

@@ -232,7 +232,7 @@ def test_walk_tuning_defaults_and_validation():
     m = modem(D)
     t = M.WalkTuning()
     M.check(M.lib().ofdm_get_walk_tuning(m.h, C.byref(t)))
-    assert (t.chunks_per_slot, t.halo_milli, t.ext_milli, t.exact_search, t.t2_f32) == (1, 2000, 0, 0, 1)
+    assert (t.chunks_per_slot, t.halo_milli, t.ext_milli, t.exact_search, t.t2_f32) == (1, 3000, 0, 0, 1)
     assert t.t2_margin == 4e-5
     with pytest.raises(M.OfdmError):
         m.walk_tuning(chunks_per_slot=0)

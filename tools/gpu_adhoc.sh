@@ -1,19 +1,9 @@
 # Scratch slot for one-off GPU commands (`gpurun -- bash tools/gpu_adhoc.sh`);
 # its content changes with the experiment at hand and is not part of any flow.
 export TMPDIR=/tmp
-R=$GRAFT_REPO_ROOT
-cd $R && mkdir -p gpurun_out
-bash tools/gpu_stream_check.sh r03p || exit 1
-bash tools/pmc_stream.sh || exit 1
-SUF=_i16 bash tools/pmc_stream.sh --i16 || exit 1
-for suf in "" _i16; do
-  alg=$(grep -h "^{" gpurun_out/pmcs_fetch$suf.log | tail -1 | python3 -c "import json,sys; print(json.loads(sys.stdin.read())['roofline']['algorithmic_bytes'])")
-  wl=$(grep -h "^{" gpurun_out/pmcs_fetch$suf.log | tail -1 | python3 -c "import json,sys; print(json.loads(sys.stdin.read())['workload'])")
-  python3 tools/pmc_stream_summary.py gpurun_out/pmc_stream$suf.json $wl $alg gpurun_out/pmc_stream_r03b$suf.json
-  grep -o '"traffic_over_algorithmic": [0-9.]*' gpurun_out/pmc_stream_r03b$suf.json
-done
-timeout -k 10 900 python bench.py --gpus 4 --backend gloo --steps 3 --warmup 1 --no-cpu-baseline --stream-reps 3 --stream-warmup 2 --no-config3 > gpurun_out/gloo4.json 2> gpurun_out/gloo4.err || exit 1
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_stream.py -k "defaults" > gpurun_out/t.log 2>&1; tail -1 gpurun_out/t.log
+timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-config3 > gpurun_out/hb.json 2> gpurun_out/hb.err || { tail gpurun_out/hb.err; exit 1; }
 python3 -c "
-import json;d=json.load(open('gpurun_out/gloo4.json'))
-for k in ('stream','stream_int16'):
-    s=d[k]; print(k, s['n_gpus'], s['frames_found'], s['rewalks_per_call'])"
+import json;d=json.load(open('gpurun_out/hb.json'))
+print(*[(k, round(d[k]['value']/1e9,1), round(d[k]['roofline']['avg_call_ms'],3), d[k]['rewalks_per_call']) for k in ('stream','stream_int16')])"
