@@ -1310,9 +1310,14 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
         // hypot of its window, as cfo_kernel does.
         constexpr int AG = 8;
         constexpr double SURE = 1.0 - 64.0 * 0x1.0p-53;
-        for (int i0 = 0; i0 <= c.P; i0 += 128 / AG) {
-            const int i = i0 + tid / AG, l = tid % AG;
-            const bool act = i <= c.P;
+        // the P windows that count (window P/2 is skipped by the sum below),
+        // 8 lanes each: for P <= 8 wave 0 alone, and a wave whose groups are
+        // all past the last window skips the pass (a uniform branch)
+        for (int g0 = 0; g0 < c.P; g0 += 128 / AG) {
+            if (g0 + w * (64 / AG) >= c.P) continue;  // uniform per wave
+            const int gi = g0 + tid / AG, l = tid % AG;
+            const int i = gi < c.P / 2 ? gi : gi + 1;
+            const bool act = gi < c.P;
             int lo = 0, hi = 0;
             if (act) {
                 lo = c.borders[i];
