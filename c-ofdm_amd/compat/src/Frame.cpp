@@ -410,12 +410,11 @@ double OFDM_FORM::pilot_freq_sinh()
         char* dr = static_cast<char*>(r.d);
         r.m->stale_lo = ch->region - r.m->host;
         r.m->stale_hi = r.m->stale_lo + ch->region_bytes;
-        check(ofdm_freq_shift(mw, (double*)dr, 1, nw, nw, ch->dcfo, st), "ofdm_freq_shift");
-        e.d2h_pinned(ch->hstate[0], dr, ch->region_bytes);
-        check(ofdm_cp_sync(mw, (double*)dr, 1, nw, nsym, st), "ofdm_cp_sync");
-        e.d2h_pinned(ch->hstate[1], dr, ch->region_bytes);
-        check(ofdm_phase_sync(mw, (double*)dr, 1, nw, nw, nullptr, 0, st), "ofdm_phase_sync");
-        e.d2h_pinned(ch->hstate[2], dr, ch->region_bytes);
+        // main.cpp:61-63 in one launch, each state written straight into its
+        // pinned copy (what output[0] holds after each member)
+        check(ofdm_sync_chain(mw, (double*)dr, 1, nw, nw, nsym, ch->dcfo, (double*)ch->hstate[0],
+                              (double*)ch->hstate[1], (double*)ch->hstate[2], 0, st),
+              "ofdm_sync_chain");
         check(ofdm_event_record(e.ctx, ch->ev[3], st), "ofdm_event_record");
         check(ofdm_chan_estimate(ch->pre_ctx->ctx, (const double*)dr, 1, ch->pre_bytes / CD, (double*)ch->dchan,
                                  ch->chan_bytes / CD, st),

@@ -1222,6 +1222,38 @@ int ofdm_phase_sync(ofdm_ctx* c, double* x, size_t nframes, size_t stride, size_
     return OFDM_OK;
 }
 
+int ofdm_sync_chain(ofdm_ctx* c, double* x, size_t nframes, size_t stride, size_t nsamples, int nsym,
+                    const double* cfo, double* shift_out, double* cp_out, double* phase_out, size_t out_stride,
+                    void* stream)
+{
+    if (!c || !x || !cfo) return fail(OFDM_ERR_INVALID, "null argument");
+    if (nsym < 1 || nsym > 64 || (size_t)c->L * nsym > nsamples) return fail(OFDM_ERR_INVALID, "bad nsym / nsamples");
+    if (nframes > 1 && stride < nsamples) return fail(OFDM_ERR_INVALID, "frame_stride < nsamples");
+    if ((size_t)c->geo.preamble_len > nsamples) return fail(OFDM_ERR_INVALID, "the preamble exceeds the form");
+    double* outs[3] = {shift_out, cp_out, phase_out};
+    for (double* o : outs)
+        if (o && nframes > 1 && out_stride < nsamples) return fail(OFDM_ERR_INVALID, "out_stride < nsamples");
+    if (!aligned16(x) || !aligned16(shift_out) || !aligned16(cp_out) || !aligned16(phase_out))
+        return fail(OFDM_ERR_INVALID, "buffers must be 16-byte aligned");
+    if (nframes == 0 || nsamples == 0) return OFDM_OK;
+    ofdm::SyncChainArgs a{};
+    a.x = reinterpret_cast<double2*>(x);
+    a.nframes = (long)nframes;
+    a.frame_stride = (long)stride;
+    a.nsamples = (long)nsamples;
+    a.cfo = cfo;
+    a.nsym = nsym;
+    a.N = c->N;
+    a.cp = c->cp;
+    a.pr = c->d_preamble;
+    a.pr_len = (long)c->geo.preamble_len;
+    for (int k = 0; k < 3; ++k) a.out[k] = reinterpret_cast<double2*>(outs[k]);
+    a.out_stride = (long)out_stride;
+    hipError_t e = ofdm::launch_sync_chain(a, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "sync_chain launch");
+    return OFDM_OK;
+}
+
 int ofdm_chan_estimate(ofdm_ctx* c, const double* x, size_t nframes, size_t stride, double* chan_out,
                        size_t chan_stride, void* stream)
 {

@@ -679,17 +679,33 @@ hipError_t launch_cfo(int logm, int g, const CfoArgs& a, hipStream_t st)
 // ========================================================================
 // freq_shift: x[n] *= exp(-2 pi i cfo n)
 // ========================================================================
+// The per-sample arithmetic of freq_shift / cp_freq_sinh / pr_phase_sinh,
+// rounded as the reference's g++ complex<double> code (no FMA): shared by the
+// three single-stage kernels and sync_chain_kernel, which equal each other
+// bit for bit.
+__device__ __forceinline__ double2 shift_sample(double2 v, double cfo, long n)
+{
+    double sn, cs;
+    sincospi(-2.0 * cfo * (double)n, &sn, &cs);
+    return cmul_exact(v, make_double2(cs, sn));
+}
+
+__device__ __forceinline__ double2 cp_rotate(double2 v, double psi, double phi, int L, int j, int N)
+{
+    const double th = -add_rn(mul_rn(psi, (double)L), mul_rn(phi, (double)j)) / N;
+    double sn, cs;
+    sincos(th, &sn, &cs);
+    return cmul_exact(v, make_double2(cs, sn));
+}
+
 __global__ void __launch_bounds__(SYNC_THREADS) freq_shift_kernel(ShiftArgs a)
 {
     const long f = blockIdx.y;
     const double cfo = a.cfo[f];
     double2* x = a.x + f * a.frame_stride;
     for (long n = blockIdx.x * (long)SYNC_THREADS + threadIdx.x; n < a.nsamples;
-         n += (long)gridDim.x * SYNC_THREADS) {
-        double sn, cs;
-        sincospi(-2.0 * cfo * (double)n, &sn, &cs);
-        x[n] = cmul(x[n], make_double2(cs, sn));
-    }
+         n += (long)gridDim.x * SYNC_THREADS)
+        x[n] = shift_sample(x[n], cfo, n);
 }
 
 hipError_t launch_freq_shift(const ShiftArgs& a, hipStream_t st)
@@ -739,10 +755,7 @@ __global__ void __launch_bounds__(CP_THREADS) cp_sync_kernel(CpArgs a)
     const long total = (long)a.nsym * L;
     for (long n = t; n < total; n += CP_THREADS) {
         const int s = (int)(n / L), j = (int)(n - (long)s * L);
-        const double th = -(psi[s] * L + phi[s] * j) / a.N;
-        double sn, cs;
-        sincos(th, &sn, &cs);
-        x[n] = cmul(x[n], make_double2(cs, sn));
+        x[n] = cp_rotate(x[n], psi[s], phi[s], L, j, a.N);
     }
 }
 
@@ -774,13 +787,124 @@ __global__ void __launch_bounds__(SYNC_THREADS) phase_sync_kernel(PhaseArgs a)
     }
     __syncthreads();
     const double2 r = rot;
-    for (long n = t; n < a.nsamples; n += SYNC_THREADS) x[n] = cmul(x[n], r);
+    for (long n = t; n < a.nsamples; n += SYNC_THREADS) x[n] = cmul_exact(x[n], r);
 }
 
 hipError_t launch_phase_sync(const PhaseArgs& a, hipStream_t st)
 {
     if (a.nframes <= 0) return hipSuccess;
     hipLaunchKernelGGL(phase_sync_kernel, dim3((unsigned)a.nframes), dim3(SYNC_THREADS), 0, st, a);
+    return hipGetLastError();
+}
+
+// ========================================================================
+// The three stages above (pilot_freq_sinh's shift, cp_freq_sinh,
+// pr_phase_sinh: main.cpp:61-63) in one workgroup per form, the form held in
+// LDS between them. Every sample, sum and angle is computed as in
+// freq_shift_kernel / cp_sync_kernel / phase_sync_kernel (the phase
+// correlation by 256 threads with block_sum2's order), so x and the stage
+// copies equal the three launches bit for bit.
+// ========================================================================
+constexpr int CHAIN_THREADS = 1024;
+constexpr long CHAIN_LDS = 158 * 1024;  // dynamic part: 160 KB less the kernel's static LDS
+
+bool sync_chain_fits(long nsamples) { return nsamples > 0 && nsamples * (long)sizeof(double2) <= CHAIN_LDS; }
+
+// IN_LDS = false (a form beyond 158 KB): the same steps on x itself, which
+// the workgroup's own barriers order (one workgroup per form).
+template <bool IN_LDS>
+__global__ void __launch_bounds__(CHAIN_THREADS) sync_chain_kernel(SyncChainArgs a)
+{
+    extern __shared__ double2 smem_chain[];
+    __shared__ double phi[64];
+    __shared__ double psi[64];
+    __shared__ double2 red[SYNC_THREADS / 64];
+    __shared__ double2 rot;
+    const long f = blockIdx.x;
+    double2* x = a.x + f * a.frame_stride;
+    double2* xs = IN_LDS ? smem_chain : x;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, L = a.N + a.cp;
+    const long ns = a.nsamples, off = f * a.out_stride;
+    const double cfo = a.cfo[f];
+    for (long n = t; n < ns; n += CHAIN_THREADS) {
+        const double2 v = shift_sample(x[n], cfo, n);
+        xs[n] = v;
+        if (a.out[0]) a.out[0][off + n] = v;
+    }
+    __syncthreads();
+    for (int s = w; s < a.nsym; s += CHAIN_THREADS / 64) {
+        double2 acc = make_double2(0.0, 0.0);
+        for (int j = lane; j < a.cp; j += 64) acc = cadd(acc, cconj_mul(xs[s * L + j], xs[s * L + j + a.N]));
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            acc.x += __shfl_xor(acc.x, o);
+            acc.y += __shfl_xor(acc.y, o);
+        }
+        if (lane == 0) phi[s] = atan2(acc.y, acc.x);
+    }
+    __syncthreads();
+    if (t == 0) {
+        double p = 0.0;
+        for (int q = 0; q < a.nsym; ++q) {
+            psi[q] = p;
+            p += phi[q];
+        }
+    }
+    __syncthreads();
+    const long total = (long)a.nsym * L;
+    for (long n = t; n < ns; n += CHAIN_THREADS) {
+        double2 v = xs[n];
+        if (n < total) {
+            const int s = (int)(n / L), j = (int)(n - (long)s * L);
+            v = cp_rotate(v, psi[s], phi[s], L, j, a.N);
+            xs[n] = v;
+        }
+        if (a.out[1]) a.out[1][off + n] = v;
+    }
+    __syncthreads();
+    // phase_sync_kernel's correlation: threads 0..255, stride 256, then the
+    // four wave sums added in wave order from 0.0 (block_sum2<256>)
+    if (t < SYNC_THREADS) {
+        double2 acc = make_double2(0.0, 0.0);
+        for (long i = t; i < a.pr_len; i += SYNC_THREADS) acc = cadd(acc, cconj_mul(a.pr[i], xs[i]));
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            acc.x += __shfl_xor(acc.x, o);
+            acc.y += __shfl_xor(acc.y, o);
+        }
+        if (lane == 0) red[w] = acc;
+    }
+    __syncthreads();
+    if (t == 0) {
+        double2 s = make_double2(0.0, 0.0);
+#pragma unroll
+        for (int i = 0; i < SYNC_THREADS / 64; ++i) s = cadd(s, red[i]);
+        double sn, cs;
+        sincos(-atan2(s.y, s.x), &sn, &cs);
+        rot = make_double2(cs, sn);
+    }
+    __syncthreads();
+    const double2 r = rot;
+    for (long n = t; n < ns; n += CHAIN_THREADS) {
+        const double2 v = cmul_exact(xs[n], r);
+        x[n] = v;
+        if (a.out[2]) a.out[2][off + n] = v;
+    }
+}
+
+hipError_t launch_sync_chain(const SyncChainArgs& a, hipStream_t st)
+{
+    if (a.nframes <= 0) return hipSuccess;
+    if (a.nsym > 64 || a.nsamples <= 0 || a.pr_len > a.nsamples || (long)a.nsym * (a.N + a.cp) > a.nsamples ||
+        a.nframes > 0x7fffffffL)
+        return hipErrorInvalidValue;
+    if (sync_chain_fits(a.nsamples)) {
+        lds_opt_in((const void*)sync_chain_kernel<true>, (int)CHAIN_LDS);
+        hipLaunchKernelGGL(sync_chain_kernel<true>, dim3((unsigned)a.nframes), dim3(CHAIN_THREADS),
+                           (size_t)a.nsamples * sizeof(double2), st, a);
+    } else {
+        hipLaunchKernelGGL(sync_chain_kernel<false>, dim3((unsigned)a.nframes), dim3(CHAIN_THREADS), 0, st, a);
+    }
     return hipGetLastError();
 }
 

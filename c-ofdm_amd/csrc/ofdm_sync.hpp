@@ -66,6 +66,20 @@ struct PhaseArgs {
     long pr_len;
 };
 
+// freq_shift -> cp_freq_sinh -> pr_phase_sinh of one form per workgroup, the
+// form held in LDS; each stage's result optionally copied to out[k] (device
+// or page-locked host memory) at out[k] + f * out_stride.
+struct SyncChainArgs {
+    double2* x;
+    long nframes, frame_stride, nsamples;
+    const double* cfo;
+    int nsym, N, cp;
+    const double2* pr;
+    long pr_len;
+    double2* out[3];
+    long out_stride;
+};
+
 struct ChanArgs {
     DevTables tab;
     const double2* x;           // preamble form
@@ -188,6 +202,8 @@ int preamble_splits(int cycles);  // workgroups per start index
 hipError_t launch_cfo(int logm, int g, const CfoArgs& a, hipStream_t st);
 hipError_t launch_freq_shift(const ShiftArgs& a, hipStream_t st);
 hipError_t launch_cp_sync(const CpArgs& a, hipStream_t st);
+hipError_t launch_sync_chain(const SyncChainArgs& a, hipStream_t st);
+bool sync_chain_fits(long nsamples);
 hipError_t launch_phase_sync(const PhaseArgs& a, hipStream_t st);
 hipError_t launch_chan(int logn, const ChanArgs& a, hipStream_t st);
 

@@ -106,6 +106,7 @@ SIGNATURES = {
     "ofdm_freq_shift": (_I, [_V, _V, _SZ, _SZ, _SZ, _V, _V]),
     "ofdm_cp_sync": (_I, [_V, _V, _SZ, _SZ, _I, _V]),
     "ofdm_phase_sync": (_I, [_V, _V, _SZ, _SZ, _SZ, _V, _SZ, _V]),
+    "ofdm_sync_chain": (_I, [_V, _V, _SZ, _SZ, _SZ, _I, _V, _V, _V, _V, _SZ, _V]),
     "ofdm_chan_estimate": (_I, [_V, _V, _SZ, _SZ, _V, _SZ, _V]),
     "ofdm_sync_frames": (_I, [_V, _V, _SZ, _SZ, _I, _V, _V, _V, _V]),
     "ofdm_rx_stream": (_I, [_V, _V, _SZ, _SZ, _L, _V, _V, _V, _V, C.POINTER(_SZ), _V]),
@@ -323,6 +324,14 @@ class Modem:
     def phase_sync(self, x, nframes: int, frame_stride: int, nsamples: int, pr=None, pr_len: int = 0,
                    stream=None):
         check(lib().ofdm_phase_sync(self.h, _ptr(x), nframes, frame_stride, nsamples, _ptr(pr), pr_len,
+                                    _stream(stream)))
+
+    def sync_chain(self, x, nframes: int, frame_stride: int, nsamples: int, nsym: int, cfo,
+                   shift_out=None, cp_out=None, phase_out=None, out_stride: int = 0, stream=None):
+        """freq_shift + cp_sync + phase_sync(context preamble) in one launch, each
+        stage's state optionally copied out."""
+        check(lib().ofdm_sync_chain(self.h, _ptr(x), nframes, frame_stride, nsamples, nsym, _ptr(cfo),
+                                    _ptr(shift_out), _ptr(cp_out), _ptr(phase_out), out_stride,
                                     _stream(stream)))
 
     def chan_estimate(self, x, nframes: int, frame_stride: int, chan_out, chan_stride: int | None = None,

@@ -295,6 +295,17 @@ int ofdm_cp_sync(ofdm_ctx* ctx, double* x, size_t nframes, size_t frame_stride, 
 int ofdm_phase_sync(ofdm_ctx* ctx, double* x, size_t nframes, size_t frame_stride,
                     size_t nsamples, const double* pr, size_t pr_len, void* stream);
 
+/* main.cpp:61-63 after the CFO estimate in one launch: ofdm_freq_shift(cfo),
+ * ofdm_cp_sync(nsym), ofdm_phase_sync(pr = NULL), in place on nsamples
+ * samples per frame (nsym*(N+cp) <= nsamples; a form up to 158 KB is held in
+ * LDS between the stages). x equals the three calls bit for bit; shift_out,
+ * cp_out, phase_out (each nullable; device or page-locked host memory from
+ * ofdm_host_alloc, frame f at + 2*f*out_stride) receive the form after each
+ * stage: the states OFDM_FORM's output[0] holds between the members. */
+int ofdm_sync_chain(ofdm_ctx* ctx, double* x, size_t nframes, size_t frame_stride, size_t nsamples,
+                    int nsym, const double* cfo, double* shift_out, double* cp_out, double* phase_out,
+                    size_t out_stride, void* stream);
+
 /* PREAMBLE_FORM::chan_char_lq (Frame.hpp:389-434): linear-phase channel
  * estimate from the preamble form at x -> chan_out[f*D .. f*D+D) unit phasors
  * (data/phases.bin layout). chan_stride: complex elements between frames. */

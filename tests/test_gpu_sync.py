@@ -112,6 +112,62 @@ def test_stagewise_sync_matches_oracle_on_golden_frame():
     assert np.abs(host(chan) - GD["phases"]).max() < 1e-10           # data/phases.bin
 
 
+@pytest.mark.parametrize("name,cfg", [("G", G), ("D", D), ("C", CC)])
+def test_sync_chain_one_launch_equals_stagewise(name, cfg):
+    """ofdm_sync_chain (freq_shift + cp_sync + phase_sync in one launch, the
+    form in LDS; config C's 720 KB form on x itself) equals the three
+    single-stage launches bit for bit, in place
+    and in each stage copy (device and page-locked host), over a batch of
+    impaired frames at frame stride; and the oracle's chain within 1e-9."""
+    m = modem(cfg)
+    g = O.geometry(cfg)
+    nf = 3
+    stream, _ = _impaired_frames(cfg, nf, seed=21 + len(name))
+    L, t2 = g["frame_len"], cfg["t2sin_size"]
+    n = g["preamble_len"] + g["message_len"]
+    nsym = cfg["num_pr_symb"] + cfg["num_symb"]
+    pre, _, _ = O.preamble_setup(cfg)
+    x0 = dev(stream)
+    cfo = torch.zeros((nf,), dtype=torch.float64, device="cuda")
+    m.cfo_estimate(x0[t2:], nf, L, cfg["num_pr_symb"], cfo)
+    ref = x0.clone()
+    states = []
+    m.freq_shift(ref[t2:], nf, L, n, cfo)
+    states.append(ref.clone())
+    m.cp_sync(ref[t2:], nf, L, nsym)
+    states.append(ref.clone())
+    m.phase_sync(ref[t2:], nf, L, n)
+    states.append(ref.clone())
+    for pinned in (False, True):
+        x = x0.clone()
+        outs = [torch.full((nf * n,), np.nan, dtype=torch.complex128, pin_memory=True) if pinned
+                else torch.full((nf * n,), np.nan, dtype=torch.complex128, device="cuda") for _ in range(3)]
+        m.sync_chain(x[t2:], nf, L, n, nsym, cfo, *outs, out_stride=n)
+        torch.cuda.synchronize()
+        assert torch.equal(x, ref)  # in place, and nothing outside the forms touched
+        for k in range(3):
+            want = torch.stack([states[k][f * L + t2: f * L + t2 + n] for f in range(nf)]).reshape(-1)
+            assert torch.equal(outs[k].cpu(), want.cpu()), (pinned, k)
+    hx, hcfo = host(x), host(cfo)
+    for f in range(nf):
+        r = stream[f * L + t2: f * L + t2 + n].copy()
+        r = O.pr_phase_sinh(O.cp_freq_sinh(cfg, O.freq_shift(r, hcfo[f])), pre)
+        assert rel_err(hx[f * L + t2: f * L + t2 + n], r) < 1e-9
+
+
+def test_sync_chain_rejects_bad_forms():
+    m = modem(G)
+    n = 1280
+    x = torch.zeros((n,), dtype=torch.complex128, device="cuda")
+    cfo = torch.zeros((1,), dtype=torch.float64, device="cuda")
+    with pytest.raises(M.OfdmError):
+        m.sync_chain(x, 1, n, 640, 2, cfo)  # nsym*(N+cp) > nsamples
+    with pytest.raises(M.OfdmError):
+        m.sync_chain(x, 1, n, n, 65, cfo)   # more symbols than one workgroup's phase table
+    with pytest.raises(M.OfdmError):
+        m.sync_chain(x, 2, n - 1, n, 2, cfo)  # frames overlap
+
+
 def test_fused_sync_and_demod_reproduce_golden_constellation():
     m = modem(G)
     x = dev(_golden_mwp())

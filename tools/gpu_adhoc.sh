@@ -3,4 +3,7 @@
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 cd $R && mkdir -p gpurun_out
-bash tools/gpu_stream_check.sh r03r && TAG=r03r LIBS="ab/base.so product" bash tools/stream_ab.sh
+timeout -k 10 600 python -u -m pytest tests/test_gpu_sync.py tests/test_dropin_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/chain_tests.log 2>&1 || { tail -60 gpurun_out/chain_tests.log; exit 1; }
+tail -3 gpurun_out/chain_tests.log
+timeout -k 10 300 python tools/dropin_rx_timing.py --frames 200 > gpurun_out/chain_dropin.json 2> gpurun_out/chain_dropin.err || { tail gpurun_out/chain_dropin.err; exit 1; }
+python3 -c "import json; d=json.load(open('gpurun_out/chain_dropin.json')); print(d['median_us'], d['frames_payload_exact'], d['stage_median_us'])"
