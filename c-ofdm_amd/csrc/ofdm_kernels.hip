@@ -833,6 +833,142 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
     leave();
 }
 
+// ------------------------------------------------------------------ rx for a few frames
+// rx_kernel spends one wave per frame and runs the frame's S transforms one
+// after another: right for thousands of frames, slow for the drop-in's one
+// frame per call (rx.cpp:211-220), whose latency is what counts there. Here a
+// workgroup holds one frame and a group of T threads per symbol (whole waves,
+// N >= 512), so the S transforms run side by side and the epilogue is spread
+// over S*T threads. Every point, gain and decision is computed by rx_kernel's
+// formulas and phys is reduced by the first T threads in rx_kernel's order,
+// so the outputs equal rx_kernel's bit for bit.
+template <int LOGN>
+__global__ void __launch_bounds__(1024) rx_wide_kernel(RxArgs a)
+{
+    using FS = FftShape<LOGN>;
+    constexpr int N = FS::N, T = FS::T;
+    extern __shared__ double2 smem[];
+    const int S = a.S, D = a.D, P = a.P;
+    double2* lds_tw = smem;                                  // TwLds::SIZE
+    double2* bufs = lds_tw + TwLds<LOGN>::SIZE;              // S ping-pong pairs (N + PADN)
+    double2* pil = bufs + (size_t)S * (N + FS::PADN);        // S*P raw pilots
+    double2* gain = pil + S * P;                             // S*P equaliser gains
+    double* red = reinterpret_cast<double*>(gain + S * P);   // 16 wave sums
+    uint8_t* dec = reinterpret_cast<uint8_t*>(red + 16);     // S*D decisions
+    const int WT = S * T, tid = threadIdx.x, s = tid / T, t = tid - s * T;
+    const long f = blockIdx.x;
+    const int L = N + a.cp;
+    double2 v[8];
+    const double2* src = a.iq + f * a.frame_stride + a.cp + (long)s * L;  // CP strip (Frame.hpp:278-279)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = load_nt(src + t + T * i);
+    load_twiddles<LOGN>(a.tab.tw, lds_tw, tid, WT);
+    int pk[RX_DPT];
+#pragma unroll
+    for (int i = 0; i < RX_DPT; ++i) pk[i] = a.tab.rx_pack[t + T * i];
+    const int pbin = a.tab.pilot_swz[t];
+    lds_barrier();
+    double2* b0 = bufs + (size_t)s * (N + FS::PADN);
+    const double2* res = fft_pp<LOGN, -1>(v, t, lds_tw, b0, b0 + N);
+    if (t < P) pil[s * P + t] = res[pbin];
+    double2 y[RX_DPT];
+#pragma unroll
+    for (int i = 0; i < RX_DPT; ++i) y[i] = res[pk[i] & 0xffff];
+    lds_barrier();
+    // phys_pilot_ampl (Frame.cpp:76-80): group 0's sum, rx_kernel's order
+    double acc = 0.0;
+    if (s == 0)
+        for (int i = t; i < S * P; i += T) acc += hypot(pil[i].x, pil[i].y);
+    acc = block_sum_lds<T>(acc, red);  // combines waves 0 .. T/64-1 only: group 0
+    const double phys = acc / ((double)(P * S) * a.pilot_ampl);
+    for (int i = tid; i < S * P; i += WT) {  // Frame.cpp:82-93
+        const int j = i % P;
+        const double2 c0 = make_double2(pil[j].x / phys, pil[j].y / phys);
+        const double2 cs = make_double2(pil[i].x / phys, pil[i].y / phys);
+        const double2 coef = cdiv_exact(cs, c0);
+        const double2 g = cdiv_exact(make_double2(1.0, 0.0), coef);
+        gain[i] = make_double2(g.x / phys, g.y / phys);
+    }
+    lds_barrier();
+    const int m = 1 << (a.k / 2);
+    const double s1 = a.k == 1 ? 0.0 : 1.0 / (2.0 / (m - 1));
+    const double2* chan = a.chan ? a.chan + f * a.chan_stride : nullptr;
+#pragma unroll
+    for (int i = 0; i < RX_DPT; ++i) {
+        const int d = t + T * i;
+        if (d >= D) continue;
+        double2 o = cmul_exact(y[i], gain[s * P + (pk[i] >> 16)]);
+        int dv;
+        if (chan) {
+            if (a.read_out) store_nt(a.read_out + (f * S + s) * D + d, o);
+            const double2 cv = load_untracked(chan + d);
+            o = a.chan_recip ? cmul_exact(o, cv) : cdiv_exact(o, cv);
+            dv = decide(o, a.k, s1, m);
+        } else {
+            dv = decide_select(o, a.k, s1, m);
+        }
+        if (a.constell) store_nt(a.constell + (f * S + s) * D + d, o);
+        dec[s * D + d] = (uint8_t)dv;
+    }
+    lds_barrier();
+    const long bpf = a.bytes_per_frame;
+    const bool by_word = (a.k == 1 || a.k == 2 || a.k == 4 || a.k == 8) && (bpf & 3) == 0 &&
+                         ((uintptr_t)a.bytes & 3) == 0 && ((uintptr_t)a.ref & 3) == 0;
+    unsigned long long errs = 0;
+    if (by_word) {
+        const int per_word = 32 / a.k;
+        for (long w = tid; w < bpf / 4; w += WT) {
+            const uint8_t* dw = dec + w * per_word;
+            uint32_t word;
+            switch (a.k) {
+                case 1: word = pack_word<1>(dw); break;
+                case 2: word = pack_word<2>(dw); break;
+                case 4: word = pack_word<4>(dw); break;
+                default: word = pack_word<8>(dw); break;
+            }
+            if (a.bytes) reinterpret_cast<uint32_t*>(a.bytes + f * bpf)[w] = word;
+            if (a.ref) errs += __popc(word ^ reinterpret_cast<const uint32_t*>(a.ref + f * bpf)[w]);
+        }
+    } else {
+        for (long jb = tid; jb < bpf; jb += WT) {
+            int byte = 0;
+            for (int b = 0; b < 8; ++b) {
+                const long bit = jb * 8 + b;
+                byte = (byte << 1) | ((dec[bit / a.k] >> (a.k - 1 - (int)(bit % a.k))) & 1);
+            }
+            if (a.bytes) a.bytes[f * bpf + jb] = (uint8_t)byte;
+            if (a.ref) errs += __popc((unsigned)(byte ^ a.ref[f * bpf + jb]));
+        }
+    }
+    if (a.bit_errors) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) errs += __shfl_xor(errs, o);
+        if ((tid & 63) == 0 && errs) atomicAdd(a.bit_errors, errs);
+    }
+}
+
+template <int LOGN>
+static size_t rx_wide_shm(const RxArgs& a)
+{
+    using FS = FftShape<LOGN>;
+    return sizeof(double2) * (TwLds<LOGN>::SIZE + (size_t)a.S * (FS::N + FS::PADN) + 2 * (size_t)a.S * a.P) +
+           16 * sizeof(double) + (size_t)a.S * a.D;
+}
+
+static int num_cus();
+
+// The few-frames form: f64 input, register-window shapes, whole-wave symbol
+// groups, and fewer frames than half the compute units (beyond that the
+// persistent rx_kernel's throughput wins). It takes no frames from a.queue,
+// whose counters stay zero.
+template <int LOGN>
+static bool rx_wide_ok(const RxArgs& a)
+{
+    constexpr int T = FftShape<LOGN>::T;
+    return LOGN >= 9 && !a.iq16 && !a.starts && !a.count && !a.ystage && a.S >= 1 &&
+           (long)a.S * T <= 1024 && a.nframes <= num_cus() / 2 && rx_wide_shm<LOGN>(a) <= 160 * 1024;
+}
+
 // ------------------------------------------------------------------ stream rx, two waves per frame
 // rx_kernel's stream mode (SYNC) for N = 512 (one transform = one wave),
 // persistent over the located frames: each frame's channel reciprocals to
@@ -1058,6 +1194,14 @@ static hipError_t rx_dispatch(const RxArgs& a, hipStream_t st, bool* staged)
     }
     if (a.iq16)
         return fits ? rx_launch_n<LOGN, false, true, false>(a, st) : rx_launch_n<LOGN, true, true, false>(a, st);
+    if constexpr (LOGN >= 9) {
+        if (fits && a.nframes > 0 && rx_wide_ok<LOGN>(a)) {
+            lds_opt_in((const void*)rx_wide_kernel<LOGN>, 160 * 1024);
+            hipLaunchKernelGGL(rx_wide_kernel<LOGN>, dim3((unsigned)a.nframes), dim3(a.S * FS::T),
+                               rx_wide_shm<LOGN>(a), st, a);
+            return hipGetLastError();
+        }
+    }
     return fits ? rx_launch_n<LOGN, false, false, false>(a, st) : rx_launch_n<LOGN, true, false, false>(a, st);
 }
 

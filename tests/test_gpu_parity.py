@@ -197,6 +197,58 @@ def test_rx_demod_read_one_launch_equals_rx_with_and_without_channel():
     assert rel_err(c, want) < 1e-14
 
 
+WIDE = ["D", "D_cp0", "D_p2", "D_qam256", "D_qam64", "D_qpsk", "D_s1", "G"]
+
+
+@pytest.mark.parametrize("name", WIDE)
+def test_few_frame_rx_equals_persistent_rx(name):
+    """rx on a few frames (one workgroup per frame, a wave per symbol: the
+    drop-in's one-frame calls) equals the persistent one-wave-per-frame rx
+    that a large batch takes, bit for bit: points, bytes, bit errors, with
+    and without a channel divisor, and rx_demod_read's pre-division points."""
+    cfg = ALL_CONFIGS[name]
+    m = modem(name)
+    g = O.geometry(cfg)
+    nf, D, bpf, npf = 300, cfg["num_data_subc"], g["bytes_per_frame"], g["npts"]
+    data = torch.from_numpy(payload(nf * bpf, seed=31)).cuda()
+    iq = torch.zeros((nf * g["message_len"],), dtype=torch.complex128, device="cuda")
+    m.tx(data, nf, iq, noise_std=0.3, seed=32)
+    rng = np.random.default_rng(33)
+    chan = dev(np.exp(1j * rng.uniform(-0.3, 0.3, nf * D)) * rng.uniform(0.8, 1.2, nf * D))
+    ref = torch.from_numpy(payload(nf * bpf, seed=34)).cuda()
+
+    def run(lo, hi, c, outs):
+        cons, byt, rd, errs = outs
+        k = hi - lo
+        msg = iq[lo * g["message_len"]:]
+        if c is None:
+            m.rx(msg, k, constell_out=cons[lo * npf:], bytes_out=byt[lo * bpf:], ref=ref[lo * bpf:], bit_errors=errs)
+        else:
+            m.rx_read(msg, k, c[lo * D:], rd[lo * npf:], chan_stride=D, constell_out=cons[lo * npf:],
+                      bytes_out=byt[lo * bpf:])
+
+    def outs():
+        return (torch.full((nf * npf,), np.nan, dtype=torch.complex128, device="cuda"),
+                torch.zeros((nf * bpf,), dtype=torch.uint8, device="cuda"),
+                torch.full((nf * npf,), np.nan, dtype=torch.complex128, device="cuda"),
+                torch.zeros((1,), dtype=torch.int64, device="cuda"))
+
+    for c in (None, chan):
+        big, few = outs(), outs()
+        run(0, nf, c, big)
+        for lo in range(0, nf, 7):
+            run(lo, min(nf, lo + 7), c, few)
+        torch.cuda.synchronize()
+        for a, b in zip(big, few):
+            if c is not None or a is not big[2]:
+                assert torch.equal(a.cpu(), b.cpu()), name
+    # and the oracle on a frame
+    f = 5
+    oc = O.ofdm_fft(cfg, host(iq)[f * g["message_len"]:(f + 1) * g["message_len"]])
+    assert rel_err(host(few[0])[f * npf:(f + 1) * npf] * np.tile(host(chan)[f * D:(f + 1) * D], cfg["num_symb"]),
+                   oc) < 1e-9
+
+
 @pytest.mark.parametrize("n", [1, 15, 16, 17, 4096, 100003])
 def test_copy_kernel_device_and_pinned(n):
     """ofdm_copy: device <-> device / page-locked host, aligned (16-B body +
