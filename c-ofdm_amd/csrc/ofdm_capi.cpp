@@ -172,8 +172,7 @@ struct ofdm_ctx {
     hipStream_t rxq_stream[RX_QUEUE_SLOTS] = {};
     int rxq_used = 0;
     ofdm_walk_tuning walk{};       // stream walker settings (ofdm_set_walk_tuning)
-    bool queue_zero = false;       // the last call's compaction resets it ...
-    hipEvent_t ev_qreset = nullptr;  // ... when this event completes
+    bool queue_zero = false;       // the last call's compaction resets it (ev_wdone marks it)
     hipEvent_t ev_walk = nullptr;  // walk records landed in h_walk
     hipEvent_t ev_wdone = nullptr;  // the walk kernel finished (caller's stream)
     hipStream_t side = nullptr;     // copies the walk records out beside the decode
@@ -326,7 +325,6 @@ int ofdm_destroy(ofdm_ctx* c)
         if (g->p) (void)hipHostFree(g->p);
     if (c->d_queue) (void)hipFree(c->d_queue);
     if (c->d_rxq) (void)hipFree(c->d_rxq);
-    if (c->ev_qreset) (void)hipEventDestroy(c->ev_qreset);
     if (c->ev_walk) (void)hipEventDestroy(c->ev_walk);
     if (c->ev_wdone) (void)hipEventDestroy(c->ev_wdone);
     if (c->side) (void)hipStreamDestroy(c->side);
@@ -1424,7 +1422,6 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     w.ncore = d_ncore;
     w.first_in = d_first_in;
     // the walkers take chunks from a queue: one resident round of workgroups
-    // drains it, slower walkers taking fewer chunks
     // drains it, slower walkers taking fewer chunks. The counter is zeroed by
     // the previous call's compaction (stream order), else here.
     if (!c->d_queue) {
@@ -1434,7 +1431,7 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     w.queue = c->d_queue;
     w.nchunks = nchunks;
     if (c->queue_zero)
-        HIP_TRY(hipStreamWaitEvent(st, c->ev_qreset, 0));  // no-op on the same stream
+        HIP_TRY(hipStreamWaitEvent(st, c->ev_wdone, 0));  // after that compaction; no-op on the same stream
     else
         HIP_TRY(hipMemsetAsync(w.queue, 0, sizeof(int), st));
     c->queue_zero = false;
@@ -1548,7 +1545,6 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     int* nrec = reinterpret_cast<int*>(ex + nchunks + 2);
     if (!c->ev_walk) HIP_TRY(hipEventCreateWithFlags(&c->ev_walk, hipEventDisableTiming));
     if (!c->ev_wdone) HIP_TRY(hipEventCreateWithFlags(&c->ev_wdone, hipEventDisableTiming));
-    if (!c->ev_qreset) HIP_TRY(hipEventCreateWithFlags(&c->ev_qreset, hipEventDisableTiming));
     if (!c->side) HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
     // Speculative decode: every chunk's in-core records, compacted on the
     // device behind the walk, are decoded while the host stitches the walks.
@@ -1584,9 +1580,9 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     HIP_TRY(hipEventRecord(c->ev_walk, c->side));
     if (spec) {
         if ((rc = decode_fused(d_pbs, ub, d_pbs + ub))) return rc;
-        // the queue counter was zeroed by the compaction: the decode is behind
-        // it in stream order, so the event can follow the decode's launch
-        HIP_TRY(hipEventRecord(c->ev_qreset, st));
+        // the queue counter was zeroed by the compaction, which ev_wdone
+        // follows: a next call on another stream waits for the compaction
+        // only, not for this decode
         c->queue_zero = true;
     }
     HIP_TRY(hipEventSynchronize(c->ev_walk));

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Experiment: the bench step (config B, 8192 frames: tx+AWGN then rx) with
 the frames in C chunks, tx of chunk k+1 on one HIP stream beside rx of chunk k
-on another (event per chunk). Prints ms per step and bit errors per C."""
+on another (event per chunk); TXRX_SEQ=1: tx(k), rx(k) in turn on one stream.
+Prints ms per step and bit errors per C."""
 import os
 import sys
 import time
@@ -32,8 +33,20 @@ noise_std = float(np.sqrt(2.0 / 10 ** 1.0))
 sa, sb = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
 
 
+SEQ = os.environ.get("TXRX_SEQ") == "1"  # one stream: tx(k), rx(k), tx(k+1), ...
+
+
 def step(C):
     per = (nf + C - 1) // C
+    if SEQ:
+        for k in range(C):
+            f0, n = k * per, min(per, nf - k * per)
+            if n <= 0:
+                break
+            modem.tx(data[f0 * bpf:], n, iq[f0 * msg:], noise_std=noise_std, seed=1, sample_offset=f0 * msg, stream=sa)
+            modem.rx(iq[f0 * msg:], n, constell_out=cons[f0 * npts:], bytes_out=out[f0 * bpf:], ref=data[f0 * bpf:],
+                     bit_errors=errs, stream=sa)
+        return
     evs = []
     for k in range(C):
         f0, n = k * per, min(per, nf - k * per)
@@ -63,4 +76,6 @@ for C in [int(c) for c in (sys.argv[1:] or ["1", "2", "4", "8", "16"])]:
         step(C)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / 20 * 1e3
+    if SEQ:
+        print("seq", end=" ")
     print(f"C={C:3d} {ms:.4f} ms/step {nf * msg / ms / 1e6:.1f} G IQ/s errs/step {int(errs.item()) // 20}", flush=True)
