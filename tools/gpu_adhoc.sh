@@ -1,11 +1,18 @@
-# Scratch slot for one-off GPU commands (`gpurun -- bash tools/gpu_adhoc.sh`);
-# its content changes with the experiment at hand and is not part of any flow.
+#!/bin/bash
+# scratch slot for one-off GPU commands (overwritten per experiment)
+# current: tx dynamic symbol queue (product build) vs HEAD (abtest/libofdm_head.so),
+# and a static tx grid-size sweep (abtest/libofdm_txgrid.so, OFDM_EXP_TX_GRID;
+# negative = that many workgroups per CU)
 export TMPDIR=/tmp
-R=$GRAFT_REPO_ROOT
-cd $R && mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_sync.py tests/test_dropin_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/wide_tests.log 2>&1 || { tail -60 gpurun_out/wide_tests.log; exit 1; }
-tail -3 gpurun_out/wide_tests.log
-timeout -k 10 300 python tools/chain_bench.py > gpurun_out/chain_bench.json 2> gpurun_out/chain_bench.err || { tail gpurun_out/chain_bench.err; exit 1; }
-cat gpurun_out/chain_bench.json
-timeout -k 10 300 python tools/dropin_rx_timing.py --frames 200 > gpurun_out/wide_dropin.json 2> gpurun_out/wide_dropin.err || { tail gpurun_out/wide_dropin.err; exit 1; }
-python3 -c "import json; d=json.load(open('gpurun_out/wide_dropin.json')); print(d['median_us'], d['frames_payload_exact'], d['stage_median_us'])"
+mkdir -p gpurun_out
+O=gpurun_out/txq.txt
+: > $O
+for rep in 1 2 3; do
+  OFDM_MI355X_LIB=abtest/libofdm_head.so timeout -k 10 120 python tools/ab_step.py 2>/dev/null | sed "s/^/head /" >> $O || exit 1
+  timeout -k 10 120 python tools/ab_step.py 2>/dev/null | sed "s/^/queue /" >> $O || exit 1
+done
+for g in -3 -6 8192 65536; do
+  OFDM_MI355X_LIB=abtest/libofdm_txgrid.so OFDM_EXP_TX_GRID=$g timeout -k 10 120 python tools/ab_step.py 2>/dev/null | sed "s/^/grid $g /" >> $O || exit 1
+done
+cat $O
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -k "tx or loopback or parity or bench or dropin" > gpurun_out/txq_tests.log 2>&1; tail -3 gpurun_out/txq_tests.log
