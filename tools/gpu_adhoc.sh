@@ -1,10 +1,15 @@
 #!/bin/bash
 # scratch slot for one-off GPU commands (overwritten per experiment)
-# current: FP32 preamble-search screen in the stream walker: the stream parity
-# tests, then a same-box A/B against HEAD's build (abtest/libofdm_head.so)
+# current: the round's final profiling pass on HEAD (headline profile + PMC, stream PMC f64/int16)
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_stream.py tests/test_gpu_stream_full.py tests/test_gpu_stream_shard.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/s32_tests.log 2>&1 || { tail -30 gpurun_out/s32_tests.log; exit 1; }
-tail -2 gpurun_out/s32_tests.log
-LIBS="abtest/libofdm_head.so product" TAG=s32 timeout -k 10 700 bash tools/stream_ab.sh || exit 1
-cat gpurun_out/s32_stream_ab.txt
+bash tools/gpu_profile_round.sh || { echo profile_round failed; exit 1; }
+bash tools/pmc_stream.sh || { echo pmc_stream failed; exit 1; }
+SUF=_i16 bash tools/pmc_stream.sh --i16 || { echo pmc_stream i16 failed; exit 1; }
+python3 -c "
+import json
+for f in ('gpurun_out/trace_timed.json','gpurun_out/pmc_rx.json','gpurun_out/pmc_tx.json','gpurun_out/pmc_stream.json','gpurun_out/pmc_stream_i16.json'):
+    print(f, json.dumps(json.load(open(f)))[:600])
+d=json.load(open('gpurun_out/bench.json'))
+print('bench', d['value']/1e9, d['ms_per_step'], d['roofline']['frac'], d['roofline']['avg_launch_ms'], d['tx_avg_launch_ms'], d['stream']['value']/1e9, d['stream_int16']['value']/1e9, d['config3']['value']/1e9)
+"
