@@ -172,7 +172,9 @@ struct ofdm_ctx {
     hipStream_t rxq_stream[RX_QUEUE_SLOTS] = {};
     int rxq_used = 0;
     ofdm_walk_tuning walk{};       // stream walker settings (ofdm_set_walk_tuning)
-    bool queue_zero = false;       // the last call's compaction resets it (ev_wdone marks it)
+    bool queue_zero = false;       // the last stream call's compaction left the walker counter zero
+    hipEvent_t ev_call = nullptr;  // the last stream call's work (every decode launch) is done
+    bool call_valid = false;       //   (ev_call recorded)
     hipEvent_t ev_walk = nullptr;  // walk records landed in h_walk
     hipEvent_t ev_wdone = nullptr;  // the walk kernel finished (caller's stream)
     hipStream_t side = nullptr;     // copies the walk records out beside the decode
@@ -325,6 +327,7 @@ int ofdm_destroy(ofdm_ctx* c)
         if (g->p) (void)hipHostFree(g->p);
     if (c->d_queue) (void)hipFree(c->d_queue);
     if (c->d_rxq) (void)hipFree(c->d_rxq);
+    if (c->ev_call) (void)hipEventDestroy(c->ev_call);
     if (c->ev_walk) (void)hipEventDestroy(c->ev_walk);
     if (c->ev_wdone) (void)hipEventDestroy(c->ev_wdone);
     if (c->side) (void)hipStreamDestroy(c->side);
@@ -1430,10 +1433,19 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     }
     w.queue = c->d_queue;
     w.nchunks = nchunks;
-    if (c->queue_zero)
-        HIP_TRY(hipStreamWaitEvent(st, c->ev_wdone, 0));  // after that compaction; no-op on the same stream
-    else
-        HIP_TRY(hipMemsetAsync(w.queue, 0, sizeof(int), st));
+    // The previous stream call's work must be done before this one rewrites
+    // the ctx's scratch (walk records, compacted list, channel): its decodes
+    // read them. On the same stream that is stream order; on another stream
+    // this call waits for the event every stream call records on exit
+    // (header: overlapping stream calls take two contexts).
+    if (!c->ev_call) HIP_TRY(hipEventCreateWithFlags(&c->ev_call, hipEventDisableTiming));
+    if (c->call_valid) HIP_TRY(hipStreamWaitEvent(st, c->ev_call, 0));  // no-op on the same stream
+    struct CallDone {  // records ev_call after everything this call enqueues
+        ofdm_ctx* c;
+        hipStream_t st;
+        ~CallDone() { c->call_valid = hipEventRecord(c->ev_call, st) == hipSuccess; }
+    } call_done{c, st};
+    if (!c->queue_zero) HIP_TRY(hipMemsetAsync(w.queue, 0, sizeof(int), st));
     c->queue_zero = false;
     hipError_t e = ofdm::launch_stream_walk(c->t2_logn, w, std::min(nchunks, slots), st);
     if (e != hipSuccess) return hip_fail(e, "stream_walk launch");
@@ -1580,9 +1592,7 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     HIP_TRY(hipEventRecord(c->ev_walk, c->side));
     if (spec) {
         if ((rc = decode_fused(d_pbs, ub, d_pbs + ub))) return rc;
-        // the queue counter was zeroed by the compaction, which ev_wdone
-        // follows: a next call on another stream waits for the compaction
-        // only, not for this decode
+        // the queue counter was zeroed by the compaction (stream order)
         c->queue_zero = true;
     }
     HIP_TRY(hipEventSynchronize(c->ev_walk));

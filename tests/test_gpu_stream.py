@@ -127,6 +127,38 @@ def test_stream_walk_fp32_t2_screen_equals_fp64(tuning):
         check_against_oracle(cfg, x, screened)
 
 
+def test_stream_calls_on_alternating_streams_one_context():
+    # one ctx, stream calls issued on two HIP streams in turn without host
+    # syncs between them: each call waits (on the device) for the previous
+    # call's decode before rewriting the ctx's scratch, so every call's
+    # outputs equal the serial call's (include/ofdm_mi355x.h stream rules)
+    x, data = impaired_stream(D, 400, seed=11)
+    mf = 512
+    ref = run_stream(D, x, max_frames=mf)
+    m = modem(D)
+    g = O.geometry(D)
+    dx = dev(x)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    bufs = [(torch.full((mf,), -1, dtype=torch.int64, device="cuda"),
+             torch.zeros((mf * g["bytes_per_frame"],), dtype=torch.uint8, device="cuda"),
+             torch.zeros((mf * g["npts"],), dtype=torch.complex128, device="cuda"),
+             torch.zeros((mf,), dtype=torch.float64, device="cuda")) for _ in range(6)]
+    torch.cuda.synchronize()  # input and zeroed outputs ready before either stream reads them
+    outs = []
+    for k, (pbs, out, cons, cfo) in enumerate(bufs):  # no host sync between the calls
+        nf = m.rx_stream(dx, len(x), mf, pb_out=pbs, bytes_out=out, constell_out=cons, cfo_out=cfo,
+                         stream=streams[k % 2])
+        outs.append((nf, pbs, out, cons, cfo))
+    torch.cuda.synchronize()
+    for nf, pbs, out, cons, cfo in outs:
+        k = min(nf, mf)
+        assert nf == ref[0]
+        assert np.array_equal(host(pbs)[:k], ref[1])
+        assert np.array_equal(host(out).reshape(mf, -1)[:k], ref[2])
+        assert np.array_equal(host(cons).reshape(mf, -1)[:k], ref[3])
+        assert np.array_equal(host(cfo)[:k], ref[4])
+
+
 def test_stream_unfused_decode_path():
     # num_symb = 12 exceeds the rx register window, so the located frames take
     # the gather + staged sync chain + staged rx path instead of the fused decode

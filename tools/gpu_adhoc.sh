@@ -1,15 +1,8 @@
 #!/bin/bash
 # scratch slot for one-off GPU commands (overwritten per experiment)
-# current: the round's final profiling pass on HEAD (headline profile + PMC, stream PMC f64/int16)
+# current: stream-call ordering across streams (per-call completion event): stream tests + stream bench
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-bash tools/gpu_profile_round.sh || { echo profile_round failed; exit 1; }
-bash tools/pmc_stream.sh || { echo pmc_stream failed; exit 1; }
-SUF=_i16 bash tools/pmc_stream.sh --i16 || { echo pmc_stream i16 failed; exit 1; }
-python3 -c "
-import json
-for f in ('gpurun_out/trace_timed.json','gpurun_out/pmc_rx.json','gpurun_out/pmc_tx.json','gpurun_out/pmc_stream.json','gpurun_out/pmc_stream_i16.json'):
-    print(f, json.dumps(json.load(open(f)))[:600])
-d=json.load(open('gpurun_out/bench.json'))
-print('bench', d['value']/1e9, d['ms_per_step'], d['roofline']['frac'], d['roofline']['avg_launch_ms'], d['tx_avg_launch_ms'], d['stream']['value']/1e9, d['stream_int16']['value']/1e9, d['config3']['value']/1e9)
-"
+timeout -k 10 600 python -u -m pytest tests/test_gpu_stream.py tests/test_gpu_stream_shard.py tests/test_bench_gpu.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/evc_tests.log 2>&1 || { tail -30 gpurun_out/evc_tests.log; exit 1; }
+tail -2 gpurun_out/evc_tests.log
+timeout -k 10 200 python tools/stream_bench.py --reps 10 > gpurun_out/evc_sb.log 2>&1 && timeout -k 10 200 python tools/stream_bench.py --reps 10 --i16 >> gpurun_out/evc_sb.log 2>&1; grep "^{" gpurun_out/evc_sb.log
