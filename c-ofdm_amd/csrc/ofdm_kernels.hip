@@ -198,8 +198,15 @@ __device__ __forceinline__ unsigned long long block_sum_u64(unsigned long long v
 // POINTS = true: FFT_FORM::write on given constellation points (no payload bytes).
 // NOISE / I16: fused AWGN and int16 wire output compiled in (a.noise_scale > 0,
 // a.iq16 != nullptr), so each variant gets its own register allocation.
+// Workgroups per CU the register allocation is bounded for: 4 at N = 2048
+// with f64 output (128 VGPRs, ~36 dwords spilled; 3 per CU at the unbounded
+// 163 VGPRs): tx 0.556 -> 0.545 ms in the bench step, same box
+// (profiles/r03z_tx_occupancy.txt). Other shapes and the int16 output keep
+// the compiler's choice.
+constexpr int tx_min_blocks(int logn, bool i16) { return logn == 11 && !i16 ? 4 : 1; }
+
 template <int LOGN, bool POINTS, bool NOISE, bool I16>
-__global__ void __launch_bounds__((1 << LOGN) / 8) tx_kernel(TxArgs a)
+__global__ void __launch_bounds__((1 << LOGN) / 8, tx_min_blocks(LOGN, I16)) tx_kernel(TxArgs a)
 {
     using FS = FftShape<LOGN>;
     constexpr int N = FS::N, T = FS::T;
