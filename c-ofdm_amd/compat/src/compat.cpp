@@ -488,8 +488,8 @@ std::vector<uint8_t> Modulation::demod(complex_vector& in)
                 std::memcpy(out.data(), ch->hbits, nb);
                 if (modulation != bpsk)  // clamped in place (modulation.cpp:70-75)
                     for (auto& z : in)
-                        z = complex_double(std::fmin(std::fmax(z.real(), -1.0), 1.0),
-                                           std::fmin(std::fmax(z.imag(), -1.0), 1.0));
+                        z = complex_double(std::clamp(z.real(), -1.0, 1.0),  // NaN stays NaN, as std::clamp
+                                           std::clamp(z.imag(), -1.0, 1.0));
                 return out;
             }
         }

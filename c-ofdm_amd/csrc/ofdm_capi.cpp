@@ -170,6 +170,7 @@ struct ofdm_ctx {
     static constexpr int RX_QUEUE_SLOTS = 32;
     int* d_rxq = nullptr;          // RX_QUEUE_SLOTS x 16 ints (one 64-B line each)
     hipStream_t rxq_stream[RX_QUEUE_SLOTS] = {};
+    bool rxq_live[RX_QUEUE_SLOTS] = {};  // slot bound to rxq_stream[i] (false: freed by ofdm_stream_destroy)
     int rxq_used = 0;
     ofdm_walk_tuning walk{};       // stream walker settings (ofdm_set_walk_tuning)
     bool queue_zero = false;       // the last stream call's compaction left the walker counter zero
@@ -617,11 +618,28 @@ int ofdm_create(const ofdm_params* params, int device, ofdm_ctx** out)
 // The rx frame-queue slot of `st` (nullptr: no slot free, static frame order).
 static int* rx_queue(ofdm_ctx* c, hipStream_t st)
 {
+    int free_slot = -1;
+    for (int i = 0; i < c->rxq_used; ++i) {
+        if (c->rxq_live[i] && c->rxq_stream[i] == st) return c->d_rxq + 16 * i;
+        if (!c->rxq_live[i] && free_slot < 0) free_slot = i;
+    }
+    if (free_slot < 0) {
+        if (c->rxq_used == ofdm_ctx::RX_QUEUE_SLOTS) return nullptr;
+        free_slot = c->rxq_used++;
+    }
+    c->rxq_stream[free_slot] = st;
+    c->rxq_live[free_slot] = true;
+    return c->d_rxq + 16 * free_slot;
+}
+
+// ofdm_stream_destroy: the stream's slot becomes free for a later stream (its
+// counters are zero once the stream has drained: the last workgroup of every
+// rx launch resets them), so a handle value reused by a new stream starts on
+// a clean slot and short-lived streams do not use the slots up.
+static void rx_queue_release(ofdm_ctx* c, hipStream_t st)
+{
     for (int i = 0; i < c->rxq_used; ++i)
-        if (c->rxq_stream[i] == st) return c->d_rxq + 16 * i;
-    if (c->rxq_used == ofdm_ctx::RX_QUEUE_SLOTS) return nullptr;
-    c->rxq_stream[c->rxq_used] = st;
-    return c->d_rxq + 16 * c->rxq_used++;
+        if (c->rxq_live[i] && c->rxq_stream[i] == st) c->rxq_live[i] = false;
 }
 
 // A launch that did not start leaves its slot as it was (zero). One that
@@ -762,7 +780,11 @@ int ofdm_stream_create(ofdm_ctx* c, void** st)
 int ofdm_stream_destroy(ofdm_ctx* c, void* st)
 {
     if (!c) return fail(OFDM_ERR_INVALID, "null ctx");
-    if (st) HIP_TRY(hipStreamDestroy((hipStream_t)st));
+    if (st) {
+        HIP_TRY(hipStreamSynchronize((hipStream_t)st));
+        rx_queue_release(c, (hipStream_t)st);
+        HIP_TRY(hipStreamDestroy((hipStream_t)st));
+    }
     return OFDM_OK;
 }
 int ofdm_memcpy_d2d(ofdm_ctx* c, void* dst, const void* src, size_t n, void* st)

@@ -116,7 +116,9 @@ __device__ __forceinline__ double2 awgn_sample(const AwgnRun& run, uint32_t j, d
 
 // awgn_sample with the scale folded into the FP32 radius (one FP32 multiply
 // instead of two FP64 ones per sample; the noise moves by ~1 FP32 ulp, far
-// inside the channel model's 1e-5 parity against the FP64 oracle)
+// inside the channel model's 1e-5 parity against the FP64 oracle). The f64 tx
+// output uses this form; the int16 wire output keeps awgn_sample's FP64
+// scale, so the two outputs' noise can differ by that ulp before truncation.
 __device__ __forceinline__ double2 awgn_sample_scaled(const AwgnRun& run, uint32_t j, float scf)
 {
     const uint32_t lo = run.lo0 + j;
@@ -906,7 +908,12 @@ __global__ void __launch_bounds__(1024) rx_wide_kernel(RxArgs a)
     double acc = 0.0;
     if (s == 0)
         for (int i = t; i < S * P; i += T) acc += hypot(pil[i].x, pil[i].y);
-    acc = block_sum_lds<T>(acc, red);  // combines waves 0 .. T/64-1 only: group 0
+    acc = block_sum_lds<T>(acc, red);  // group 0's sum in group 0's threads
+    // broadcast it: at T = 64 block_sum_lds is the wave's own shuffle sum, so
+    // the other groups (tid >= T) hold their own zero sums
+    if (tid == 0) red[15] = acc;
+    lds_barrier();
+    acc = red[15];
     const double phys = acc / ((double)(P * S) * a.pilot_ampl);
     for (int i = tid; i < S * P; i += WT) {  // Frame.cpp:82-93
         const int j = i % P;

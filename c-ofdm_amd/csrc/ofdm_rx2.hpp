@@ -12,9 +12,14 @@
 // 2 at 256 VGPRs), each frame transformed by two waves at once (one LDS
 // image per wave; the transforms sync within their wave). No prefetch
 // registers: the other waves of the SIMD cover the load latency. The
-// operations are rx_kernel's, one for one: the phase ramp, the transform,
-// phys (wave 0, the same lane order), the gains, the channel reciprocal
-// multiply (chan_recip mode; D <= 256), the decisions.
+// operations are rx_kernel's (the phase ramp, the transform, phys in wave 0's
+// lane order, the channel reciprocal multiply in chan_recip mode with
+// D <= 256, the decisions) with one rounding difference: the gains are
+// c0*conj(cs) / (|cs|^2 phys), one division, where rx_kernel keeps the
+// reference's two Smith divisions (Frame.cpp:82-93). The stream points are
+// therefore not bit-identical to batch rx; they are held to the oracle at
+// 1e-9 relative with bit-exact decisions (tests/common.py
+// check_stream_frames), the same bar as the rest of the sync chain.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>

@@ -54,6 +54,7 @@ EXTRA = {
     "D_s1": cfg(O.DEFAULT, num_symb=1),
     "D_p2": cfg(O.DEFAULT, num_pilot_subc=2),
     "D_cp0": cfg(O.DEFAULT, cp_size=0),
+    "D_p16": cfg(O.DEFAULT, num_pilot_subc=16),  # S*P = 128 > 64: rx_wide_kernel's phys broadcast
 }
 ALL_CONFIGS = {"D": D, "G": G, "B": B, "C": CC, **EXTRA}
 
@@ -100,14 +101,16 @@ def distance_to_threshold(k, pts):
     return np.minimum(dre, dim)
 
 
-def check_stream_frames(cfg, x, pbs, got_bytes, got_cons, got_cfo=None, tol=1e-9):
+def check_stream_frames(cfg, x, pbs, got_bytes, got_cons, got_cfo=None, tol=1e-9, allow_flips=False):
     """Every located frame of a stream against the oracle's main.cpp:60-80
     chain on the same samples (orc_decode_frames): CFO exact, constellation
     within `tol` relative per frame, and every byte equal, except that a
     decision may differ where the oracle's own point lies within the rounding
     band of its threshold (twice the largest GPU-oracle point difference of
     the whole stream: the sync chain's transcendentals and the FFT round
-    differently). Returns a summary dict (printed by callers)."""
+    differently). With allow_flips False (the default) no
+    decision may differ at all: north_star's bit-exact decisions. Returns a
+    summary dict."""
     k = cfg["mod_type"]
     g = O.geometry(cfg)
     nf = len(pbs)
@@ -130,6 +133,7 @@ def check_stream_frames(cfg, x, pbs, got_bytes, got_cons, got_cfo=None, tol=1e-9
         worst = max(worst, float(d.max()))
         assert np.all(d <= band), (f"frame {f}: {len(pts)} decisions differ, farthest {d.max():.3e} "
                                    f"from its threshold (band {band:.3e})")
+    assert allow_flips or flips == 0, f"{flips} decisions differ from the oracle on {diff_frames.size} frames"
     return {"frames": nf, "max_constellation_rel_err": float(err.max()), "band": band,
             "frames_with_flips": int(diff_frames.size), "decision_flips": flips,
             "farthest_flip_from_threshold": worst}

@@ -197,7 +197,7 @@ def test_rx_demod_read_one_launch_equals_rx_with_and_without_channel():
     assert rel_err(c, want) < 1e-14
 
 
-WIDE = ["D", "D_cp0", "D_p2", "D_qam256", "D_qam64", "D_qpsk", "D_s1", "G"]
+WIDE = ["D", "D_cp0", "D_p2", "D_p16", "D_qam256", "D_qam64", "D_qpsk", "D_s1", "G"]
 
 
 @pytest.mark.parametrize("name", WIDE)
