@@ -167,7 +167,7 @@ def cpu_stream_baseline(p, x_host: np.ndarray, budget_s: float, i16: bool = Fals
             h = w[0::2] + 1j * w[1::2]
         else:
             h = x_host[:n]
-        pbs = O.stream_walk(p, h)
+        pbs = O.stream_walk_ring(p, h)[0]  # rx.cpp's walk with its SDR ring
         for pb in pbs:
             if pb + span <= len(h):
                 O.decode_frame(p, h[pb:pb + span])
@@ -177,7 +177,7 @@ def cpu_stream_baseline(p, x_host: np.ndarray, budget_s: float, i16: bool = Fals
         n = min(total, n * 4)
     conv = "int16 -> f64 conversion + " if i16 else ""
     return {"value": n / dt, "unit": "stream samples/s", "cores": 1, "kind": "port",
-            "sample": f"{conv}oracle orc_stream_walk + orc_decode_frame (own FFT; FFTW absent) over the first {n} "
+            "sample": f"{conv}oracle orc_stream_walk_ring + orc_decode_frame (own FFT; FFTW absent) over the first {n} "
                       f"samples ({len(pbs)} frames) of the same stream in {dt:.1f} s, 1 thread "
                       f"(rx.cpp's loop is single-threaded) on {_cpu_model()}"}
 
@@ -199,7 +199,8 @@ def stream_leg(args, dist, dev, world, rank, M, i16: bool):
     p = dict(CONFIG_D)
     modem = M.Modem(p, dev.index)
     layout = Y.StreamLayout(p, args.stream_frames * world)
-    rx = SS.ShardedStreamRx(p, layout.n, world, rank)
+    # rx.cpp's SDR ring (the config's rx_buf_size, the library's default) and initial state
+    rx = SS.ShardedStreamRx(p, layout.n, world, rank, ring=modem.stream_ring(), initial=modem.initial_state())
     nsl = rx.slice_hi - rx.slice_lo
     x = Y.stream_slice(modem, layout, rx.slice_lo, rx.slice_hi, dev, i16=i16)
     f0, f1 = layout.frames_overlapping(rx.slice_lo, rx.slice_hi)
@@ -300,7 +301,7 @@ def stream_pipelined(args, p, M, dev, modem, layout, rx, walk, outs, x, nsl, cap
         m2 = M.Modem(p, dev.index)
         st2 = torch.cuda.Stream(dev)
         o2 = {k: torch.empty_like(v) for k, v in outs.items()}
-        r2 = SS.ShardedStreamRx(p, layout.n, 1, 0)
+        r2 = SS.ShardedStreamRx(p, layout.n, 1, 0, ring=m2.stream_ring(), initial=m2.initial_state())
         mods.append(m2)
         sts.append(st2)
         outl.append(o2)

@@ -173,6 +173,7 @@ struct ofdm_ctx {
     bool rxq_live[RX_QUEUE_SLOTS] = {};  // slot bound to rxq_stream[i] (false: freed by ofdm_stream_destroy)
     int rxq_used = 0;
     ofdm_walk_tuning walk{};       // stream walker settings (ofdm_set_walk_tuning)
+    long ring = 0;                 // rx.cpp's SDR ring R (ofdm_set_stream_ring; 0: the continuous walk)
     bool queue_zero = false;       // the last stream call's compaction left the walker counter zero
     hipEvent_t ev_call = nullptr;  // the last stream call's work (every decode launch) is done
     bool call_valid = false;       //   (ev_call recorded)
@@ -611,6 +612,7 @@ int ofdm_create(const ofdm_params* params, int device, ofdm_ctx** out)
         return hip_fail(qe, "rx frame counters");
     }
     ofdm_walk_tuning_default(&c->walk);
+    c->ring = std::max(0L, c->p.rx_buf_size) * c->geo.frame_len;  // rx.cpp:53 / sdr.hpp:141
     *out = c;
     return OFDM_OK;
 }
@@ -1342,20 +1344,37 @@ int ofdm_sync_frames(ofdm_ctx* c, double* frames, size_t nframes, size_t stride,
 
 }  // extern "C"
 
+// rx.cpp's initial walk state (rx.cpp:105-114): pos = 0 of a buffer whose
+// first output_size samples are the zero header before the first SDR buffer,
+// i.e. stream position -output_size in a ring ending at R; the continuous
+// walk starts at the stream's first sample.
+static ofdm_walk_state initial_state(const ofdm_ctx* c)
+{
+    return c->ring > 0 ? ofdm_walk_state{-c->geo.frame_len, c->ring} : ofdm_walk_state{0, 0};
+}
+
 // ofdm_rx_stream / ofdm_rx_stream_i16 / ofdm_rx_stream_shard: exactly one of
 // iq, iq16 is set. The walk starts at state `start`; frames located with pb in
 // [own_lo, own_hi) are decoded (the whole stream: start = own_lo = 0, own_hi = n).
 static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, size_t n, size_t max_frames,
                           long chunk, long* pb_out, uint8_t* bytes_out, double* constell_out, double* cfo_out,
-                          size_t* nframes_out, void* stream, long start, long own_lo, long own_hi,
-                          long* located, size_t located_cap, size_t* nlocated_out, long* exit_out)
+                          size_t* nframes_out, void* stream, ofdm_walk_state start_state, long own_lo, long own_hi,
+                          long* located, uint8_t* located_lag, size_t located_cap, size_t* nlocated_out,
+                          ofdm_walk_state* exit_out)
 {
     if (!c || (!iq && !iq16) || !nframes_out) return fail(OFDM_ERR_INVALID, "null argument");
     *nframes_out = 0;
     if (nlocated_out) *nlocated_out = 0;
-    if (exit_out) *exit_out = -1;
-    if (start < 0 || own_lo < 0 || own_lo > own_hi || own_hi > (long)n)
-        return fail(OFDM_ERR_INVALID, "need 0 <= start, 0 <= own_lo <= own_hi <= n");
+    if (exit_out) *exit_out = ofdm_walk_state{-1, 0};
+    const long R = c->ring, flen0 = c->geo.frame_len;
+    const long start = start_state.pos;
+    // ring mode: the walk may start in rx.cpp's zero header before the first
+    // SDR buffer ([-output_size, 0)); its ring end lies ahead of it, within R
+    if (R > 0 ? (start < -flen0 || start_state.ring_end <= start || start_state.ring_end > start + R + flen0)
+              : start < 0)
+        return fail(OFDM_ERR_INVALID, "start state out of range (ring mode: -output_size <= pos < ring_end <= pos + R + output_size)");
+    if (own_lo < 0 || own_lo > own_hi || own_hi > (long)n)
+        return fail(OFDM_ERR_INVALID, "need 0 <= own_lo <= own_hi <= n");
     if (c->t2_logn < 6 || c->t2_logn > 11) return fail(OFDM_ERR_UNSUPPORTED, "stream walk needs T2sin_size = 2^a, 64..2048");
     if ((iq && !aligned16(iq)) || (iq16 && ((uintptr_t)iq16 & 3)) || (constell_out && !aligned16(constell_out)))
         return fail(OFDM_ERR_INVALID, "misaligned buffer (complex<double> 16 B, complex<int16> 4 B)");
@@ -1392,13 +1411,15 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
                c->p.pr_sin_len) / msg + 4);
     int rc;
     const size_t rec_b = (size_t)nchunks * max_rec * sizeof(long);
-    const size_t walk_b0 = rec_b + (size_t)nchunks * (sizeof(long) + sizeof(int)) + 2 * sizeof(long) + 64;
+    // layout: records | exit states | exit ring ends | re-walk start (pos, ring end) | counts | ...
+    const size_t walk_b0 = rec_b + (size_t)nchunks * (2 * sizeof(long) + sizeof(int)) + 2 * sizeof(long) + 64;
     const size_t walk_b = walk_b0 + 2 * (size_t)nchunks * sizeof(int);  // + in-core counts and first indices
     if ((rc = grow(c, c->s_walk, walk_b))) return rc;
     char* wb = static_cast<char*>(c->s_walk.p);
     long* d_rec = reinterpret_cast<long*>(wb);
     long* d_exit = reinterpret_cast<long*>(wb + rec_b);
-    long* d_start = d_exit + nchunks;  // one re-walk start
+    long* d_exit_ring = d_exit + nchunks;
+    long* d_start = d_exit_ring + nchunks;  // one re-walk start state (pos, ring end)
     int* d_nrec = reinterpret_cast<int*>(d_start + 2);
     int* d_ids = d_nrec + nchunks;     // one re-walk chunk id (in the 64 B slack)
     int* d_ncore = reinterpret_cast<int*>(wb + walk_b0);
@@ -1431,6 +1452,11 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     w.chunk = chunk;
     w.halo = halo;
     w.start = start;
+    w.ring = R;
+    w.out_len = flen;
+    w.start_ring_end = start_state.ring_end;
+    w.ring_phase = R > 0 ? ((start_state.ring_end % R) + R) % R : 0;
+    w.exit_ring = d_exit_ring;
     w.core_lo = own_lo;
     w.core_hi = own_hi;
     w.ext = ext;
@@ -1576,7 +1602,8 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     char* hb = static_cast<char*>(c->h_walk.p);
     long* rec = reinterpret_cast<long*>(hb);
     long* ex = reinterpret_cast<long*>(hb + rec_b);
-    int* nrec = reinterpret_cast<int*>(ex + nchunks + 2);
+    long* exr = ex + nchunks;
+    int* nrec = reinterpret_cast<int*>(exr + nchunks + 2);
     if (!c->ev_walk) HIP_TRY(hipEventCreateWithFlags(&c->ev_walk, hipEventDisableTiming));
     if (!c->ev_wdone) HIP_TRY(hipEventCreateWithFlags(&c->ev_wdone, hipEventDisableTiming));
     if (!c->side) HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
@@ -1620,12 +1647,15 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     HIP_TRY(hipEventSynchronize(c->ev_walk));
 
     // the speculative list, from the walks as they came back
+    // a record's preamble start (ring mode: the lag bit stripped; a frame
+    // before the stream's first sample stays negative)
+    auto rec_pb = [](long r) { return r < 0 ? r : (r & ofdm::WALK_REC_PB); };
     std::vector<long> spec_list;
     if (spec)
         for (long k = 0; k < nchunks; ++k) {
             const long lo = own_lo + k * chunk, hi = std::min(lo + chunk, own_hi);
             for (int i = 0; i < std::min(nrec[k], max_rec); ++i) {
-                const long pb = rec[(size_t)k * max_rec + i];
+                const long pb = rec_pb(rec[(size_t)k * max_rec + i]);
                 if (pb >= lo && pb < hi) spec_list.push_back(pb);
             }
         }
@@ -1636,12 +1666,14 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     // frame (from there on both are the same computation); otherwise it is
     // re-walked from the previous exit state (exact), with one workgroup.
     long nrewalk = 0;
-    auto rewalk = [&](long k, long start) -> int {
+    auto rewalk = [&](long k, long start, long start_ring) -> int {
         ofdm::WalkArgs r = w;
         const int id = (int)k;
-        HIP_TRY(hipMemcpyAsync(d_start, &start, sizeof(long), hipMemcpyHostToDevice, st));
+        const long st2[2] = {start, start_ring};
+        HIP_TRY(hipMemcpyAsync(d_start, st2, sizeof(st2), hipMemcpyHostToDevice, st));
         HIP_TRY(hipMemcpyAsync(d_ids, &id, sizeof(int), hipMemcpyHostToDevice, st));
         r.start_pos = d_start;
+        r.start_ring = d_start + 1;
         r.chunk_ids = d_ids;
         r.queue = nullptr;
         ++nrewalk;
@@ -1650,13 +1682,17 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
         HIP_TRY(hipMemcpyAsync(rec + (size_t)k * max_rec, d_rec + (size_t)k * max_rec, max_rec * sizeof(long),
                                hipMemcpyDeviceToHost, st));
         HIP_TRY(hipMemcpyAsync(&ex[k], d_exit + k, sizeof(long), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(&exr[k], d_exit_ring + k, sizeof(long), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipMemcpyAsync(&nrec[k], d_nrec + k, sizeof(int), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         return OFDM_OK;
     };
-    std::vector<long> frames, walk_in;
-    std::vector<long> prev;  // every frame the accepted walk of the previous chunk located
-    long texit = 0, last_k = -1;
+    // records compare whole (preamble start and, in ring mode, the ring of the
+    // state after the frame): equal records = equal walks from there on
+    std::vector<long> frames, walk_in;  // frames: preamble starts; walk_in: records
+    std::vector<long> owned_rec;        // the owned frames' records
+    std::vector<long> prev;  // every record of the accepted walk of the previous chunk
+    long texit = 0, texit_ring = start_state.ring_end, last_k = -1;
     for (long k = 0; k < nchunks; ++k) {
         if (k > 0 && texit < 0) break;  // the true walk ended
         if (nrec[k] > max_rec) return fail(OFDM_ERR_HIP, "stream walk record overflow");
@@ -1664,45 +1700,61 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
         const long lo = own_lo + k * chunk, hi = std::min(lo + chunk, own_hi);
         if (k > 0) {
             long first_owned = LONG_MAX;
-            for (long pb : lst)
-                if (pb >= lo && pb < hi) first_owned = std::min(first_owned, pb);
+            for (long r : lst)
+                if (rec_pb(r) >= lo && rec_pb(r) < hi) first_owned = std::min(first_owned, rec_pb(r));
             bool sync = false;
-            for (long pb : lst)
-                if (pb <= first_owned && std::find(prev.begin(), prev.end(), pb) != prev.end()) sync = true;
+            for (long r : lst)
+                if (rec_pb(r) <= first_owned && std::find(prev.begin(), prev.end(), r) != prev.end()) sync = true;
             if (!sync) {
                 if (getenv("OFDM_STREAM_DEBUG")) {
-                    fprintf(stderr, "ofdm_rx_stream: re-walk chunk %ld [%ld, %ld) from %ld; its walk:", k, lo, hi, texit);
-                    for (long pb : lst) fprintf(stderr, " %ld", pb);
+                    fprintf(stderr, "ofdm_rx_stream: re-walk chunk %ld [%ld, %ld) from (%ld, %ld); its walk:", k, lo, hi,
+                            texit, texit_ring);
+                    for (long r : lst) fprintf(stderr, " %ld%s", rec_pb(r), r > 0 && (r & ofdm::WALK_REC_LAG) ? "+" : "");
                     fprintf(stderr, " | previous:");
-                    for (long pb : prev) fprintf(stderr, " %ld", pb);
+                    for (long r : prev) fprintf(stderr, " %ld%s", rec_pb(r), r > 0 && (r & ofdm::WALK_REC_LAG) ? "+" : "");
                     fprintf(stderr, "\n");
                 }
-                if ((rc = rewalk(k, texit))) return rc;
+                if ((rc = rewalk(k, texit, texit_ring))) return rc;
                 if (nrec[k] > max_rec) return fail(OFDM_ERR_HIP, "stream walk record overflow");
                 lst.assign(rec + (size_t)k * max_rec, rec + (size_t)k * max_rec + nrec[k]);
             }
         }
         if (k == 0)  // the walk-in from `start` (true by definition): frames before own_lo
-            for (long pb : lst)
-                if (pb < lo) walk_in.push_back(pb);
-        for (long pb : lst)
-            if (pb >= lo && pb < hi) frames.push_back(pb);
+            for (long r : lst)
+                if (rec_pb(r) < lo) walk_in.push_back(r);
+        for (long r : lst)
+            if (rec_pb(r) >= lo && rec_pb(r) < hi) {
+                frames.push_back(rec_pb(r));
+                owned_rec.push_back(r);
+            }
         prev.swap(lst);
         texit = ex[k];
+        texit_ring = exr[k];
         last_k = k;
     }
+    // rx.cpp decodes a frame whose preamble the ring's zero header precedes
+    // (pb < 0: the capture starts inside a frame's preamble); the stream API's
+    // outputs index the caller's samples, so it reports the case instead
+    for (long r : walk_in)
+        if (r < 0)
+            return fail(OFDM_ERR_UNSUPPORTED, "a frame starts %ld samples before the stream's first sample "
+                                              "(rx.cpp's ring would decode it from its zero header)", -r);
     *nframes_out = frames.size();
-    if (exit_out) *exit_out = last_k == nchunks - 1 ? texit : -1;
+    if (exit_out && last_k == nchunks - 1) *exit_out = ofdm_walk_state{texit, texit < 0 ? 0 : texit_ring};
     if (nlocated_out) {
         // every frame of the stitched walk: the walk-in, the owned frames, and
         // what the last walker located past own_hi before it stopped
         std::vector<long> all(walk_in);
-        all.insert(all.end(), frames.begin(), frames.end());
+        all.insert(all.end(), owned_rec.begin(), owned_rec.end());
         if (last_k == nchunks - 1)
-            for (long pb : prev)
-                if (pb >= own_hi) all.push_back(pb);
+            for (long r : prev)
+                if (rec_pb(r) >= own_hi) all.push_back(r);
         *nlocated_out = all.size();
-        if (located) std::memcpy(located, all.data(), std::min(all.size(), located_cap) * sizeof(long));
+        const size_t nl = std::min(all.size(), located_cap);
+        for (size_t i = 0; i < nl; ++i) {
+            if (located) located[i] = rec_pb(all[i]);
+            if (located_lag) located_lag[i] = all[i] > 0 && (all[i] & ofdm::WALK_REC_LAG) ? 1 : 0;
+        }
     }
     if (getenv("OFDM_STREAM_DEBUG"))
         fprintf(stderr, "ofdm_rx_stream: %ld chunks of %ld samples, halo %ld, %ld re-walks, %zu frames, speculative %s\n",
@@ -1759,7 +1811,7 @@ int ofdm_rx_stream(ofdm_ctx* c, const double* iq, size_t n, size_t max_frames, l
 {
     if (!iq) return fail(OFDM_ERR_INVALID, "null argument");
     return rx_stream_impl(c, iq, nullptr, n, max_frames, chunk, pb_out, bytes_out, constell_out, cfo_out,
-                          nframes_out, stream, 0, 0, (long)n, nullptr, 0, nullptr, nullptr);
+                          nframes_out, stream, initial_state(c), 0, (long)n, nullptr, nullptr, 0, nullptr, nullptr);
 }
 
 int ofdm_rx_stream_i16(ofdm_ctx* c, const int16_t* iq16, size_t n, size_t max_frames, long chunk, long* pb_out,
@@ -1767,7 +1819,7 @@ int ofdm_rx_stream_i16(ofdm_ctx* c, const int16_t* iq16, size_t n, size_t max_fr
 {
     if (!iq16) return fail(OFDM_ERR_INVALID, "null argument");
     return rx_stream_impl(c, nullptr, iq16, n, max_frames, chunk, pb_out, bytes_out, constell_out, cfo_out,
-                          nframes_out, stream, 0, 0, (long)n, nullptr, 0, nullptr, nullptr);
+                          nframes_out, stream, initial_state(c), 0, (long)n, nullptr, nullptr, 0, nullptr, nullptr);
 }
 
 int ofdm_stream_shard_margins(const ofdm_ctx* c, long* halo_out, long* tail_out)
@@ -1809,14 +1861,39 @@ int ofdm_set_walk_tuning(ofdm_ctx* c, const ofdm_walk_tuning* t)
     return OFDM_OK;
 }
 
-int ofdm_rx_stream_shard(ofdm_ctx* c, const double* iq, const int16_t* iq16, size_t n, long start, long own_lo,
-                         long own_hi, size_t max_frames, long chunk, long* pb_out, uint8_t* bytes_out,
+int ofdm_rx_stream_shard(ofdm_ctx* c, const double* iq, const int16_t* iq16, size_t n, const ofdm_walk_state* start,
+                         long own_lo, long own_hi, size_t max_frames, long chunk, long* pb_out, uint8_t* bytes_out,
                          double* constell_out, double* cfo_out, size_t* nframes_out, long* located,
-                         size_t located_cap, size_t* nlocated_out, long* exit_out, void* stream)
+                         uint8_t* located_lag, size_t located_cap, size_t* nlocated_out, ofdm_walk_state* exit_out,
+                         void* stream)
 {
     if (!iq == !iq16) return fail(OFDM_ERR_INVALID, "exactly one of iq, iq16");
-    return rx_stream_impl(c, iq, iq16, n, max_frames, chunk, pb_out, bytes_out, constell_out, cfo_out,
-                          nframes_out, stream, start, own_lo, own_hi, located, located_cap, nlocated_out, exit_out);
+    if (!c || !start) return fail(OFDM_ERR_INVALID, "null argument");
+    return rx_stream_impl(c, iq, iq16, n, max_frames, chunk, pb_out, bytes_out, constell_out, cfo_out, nframes_out,
+                          stream, *start, own_lo, own_hi, located, located_lag, located_cap, nlocated_out, exit_out);
+}
+
+int ofdm_stream_initial_state(const ofdm_ctx* c, ofdm_walk_state* out)
+{
+    if (!c || !out) return fail(OFDM_ERR_INVALID, "null argument");
+    *out = initial_state(c);
+    return OFDM_OK;
+}
+
+int ofdm_set_stream_ring(ofdm_ctx* c, long ring)
+{
+    if (!c) return fail(OFDM_ERR_INVALID, "null ctx");
+    if (ring < 0 || (ring > 0 && ring < 2 * c->geo.frame_len))
+        return fail(OFDM_ERR_INVALID, "ring must be 0 or at least 2 * output_size (rx.cpp's buffer holds output_size + R)");
+    c->ring = ring;
+    return OFDM_OK;
+}
+
+int ofdm_get_stream_ring(const ofdm_ctx* c, long* ring)
+{
+    if (!c || !ring) return fail(OFDM_ERR_INVALID, "null argument");
+    *ring = c->ring;
+    return OFDM_OK;
 }
 
 }  // extern "C"

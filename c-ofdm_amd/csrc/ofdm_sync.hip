@@ -1933,6 +1933,17 @@ __device__ __forceinline__ void load8_block(const A& a, long base, bool live, do
     }
 }
 
+// x[base + T*i], i < 8, for a block that straddles the stream's ends (ring
+// mode: rx.cpp's zero header before the first SDR buffer, the zeros after a
+// capture): samples outside [0, n) read as zero. Rare (a walk's first and
+// last blocks), so per-sample guards are fine here.
+template <int T, class A>
+__device__ __forceinline__ void load8_block_part(const A& a, long base, double2 (&v)[8])
+{
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = stream_sample(a, base + T * i);
+}
+
 __device__ __forceinline__ double energy_rn(double2 v) { return add_rn(mul_rn(v.x, v.x), mul_rn(v.y, v.y)); }
 
 // load8_block rounded to FP32 (int16 wire samples convert exactly).
@@ -2325,8 +2336,20 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
     // start state, the others from a halo before their core
     const long core0 = a.core_lo + (long)c * a.chunk, end = min(core0 + a.chunk, a.core_hi);
     long pos = a.start_pos ? a.start_pos[blockIdx.x] : (c == 0 ? a.start : (core0 > a.halo ? core0 - a.halo : 0));
+    const bool ring = a.ring > 0;  // uniform
+    // ring mode: the first ring end after position q (the ring ends lie on
+    // ring_phase + k*ring)
+    auto ring_after = [&](long q) -> long {
+        const long d = q - a.ring_phase;
+        const long k = d >= 0 ? d / a.ring : -((-d + a.ring - 1) / a.ring);  // floor(d / ring)
+        return a.ring_phase + (k + 1) * a.ring;
+    };
+    // the start state's ring end: given (chunk 0, re-walks), else the first
+    // ring end after the halo start (a guess; the host's stitching checks it)
+    long rend = 0;
+    if (ring) rend = a.start_pos ? a.start_ring[blockIdx.x] : (c == 0 ? a.start_ring_end : ring_after(pos));
     int nrec = 0, ncore = 0, first_in = 0;
-    long exitp = -1;
+    long exitp = -1, exitr = 0;
     bool past = false;  // a frame at or past the core end is located
     __syncthreads();
     for (;;) {
@@ -2343,10 +2366,13 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
         // the next chunk's first frame is in this chunk's records whenever the
         // two walks agree: a short halo then suffices to meet the true walk.
         if (pos >= end) {
-            if (exitp < 0) exitp = pos;
+            if (exitp < 0) {
+                exitp = pos;
+                exitr = rend;
+            }
             if (past || pos >= end + a.ext) break;
         }
-        const long spos = pos;  // this step's start state
+        const long spos = pos, srend = rend;  // this step's start state
         {
             // issue priority by the work left: walkers further from their
             // core end go first. The arbiter otherwise favours the oldest
@@ -2376,9 +2402,14 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
             int tt;
             asm volatile("v_mov_b32 %0, %1" : "=v"(tt) : "v"(tt0));
             const long b = base + (long)g * N;
-            const bool live = b + N <= a.n;
+            // a block is tested when it lies in the stream (ring mode: in the
+            // ring, data or zeros; blocks wholly past n are zeros and never hit)
+            const bool live = ring ? (b + N <= rend && b < a.n) : b + N <= a.n;
             double2 v[8];
-            load8_block<T>(a, b + tt, live, v);
+            if (ring && live && (b < 0 || b + N > a.n))
+                load8_block_part<T>(a, b + tt, v);
+            else
+                load8_block<T>(a, b + tt, live, v);
             // the last pass stays in registers: v[i] = X[tt + T*i], the bins
             // this thread sums (no final LDS write, barrier and re-read); a
             // transform of T <= 64 threads lies within one wave, so its LDS
@@ -2424,17 +2455,26 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
             ++scan_it;
             return bg;
         };
-        // stop checks of a scan step from `base` (the walk state is `base`)
-        auto scan_stop = [&](long base) -> bool {
-            if (base + N > a.n) return true;  // no full block left: the walk has consumed the stream
+        // checks before a scan step from `base` (the walk state is (base, rend)):
+        // 1 = stop, 2 = ring exhausted (rx.cpp:137-145: refill without carry,
+        // the grid restarts at the next buffer), 0 = scan
+        bool miss = false;
+        auto scan_stop = [&](long base) -> int {
+            // no full block left / (ring) the scan is past the capture, whose
+            // zeros never hit: the walk has consumed the stream
+            if (ring ? base >= a.n : base + N > a.n) return 1;
             if (base >= end) {                // scanning past the core: an equivalent state
-                if (exitp < 0) exitp = base;
+                if (exitp < 0) {
+                    exitp = base;
+                    exitr = rend;
+                }
                 // the end fell inside a scan: walk on to the next located frame
                 // (within ext_scan), so that the next chunk's walk, which
                 // locates it too, syncs with this one without a re-walk
-                if (base >= end + a.ext_scan) return true;
+                if (base >= end + a.ext_scan) return 1;
             }
-            return false;
+            if (ring && base + N > rend) return 2;  // find_t2sin's blocks end with the buffer
+            return 0;
         };
         if constexpr (T <= 64) {
             if (a.t2_f32) {
@@ -2449,19 +2489,33 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
                 float4* fftb32 = reinterpret_cast<float4*>(big);  // one image per group, both blocks
                 const float lev = (float)a.t2_level, marg = (float)a.t2_margin;
                 for (long base = pos;; base += 2L * G * N) {
-                    if (scan_stop(base)) {
-                        stop = true;
+                    if (const int ss = scan_stop(base)) {
+                        stop = ss == 1;
+                        miss = ss == 2;
                         break;
                     }
                     int tt;  // opaque per-step copy (see t2_eval64)
                     asm volatile("v_mov_b32 %0, %1" : "=v"(tt) : "v"(tt0));
                     const long bA = base + (long)g * N, bB = bA + (long)G * N;
-                    const bool liveA = bA + N <= a.n, liveB = bB + N <= a.n;
+                    const bool liveA = ring ? (bA + N <= rend && bA < a.n) : bA + N <= a.n;
+                    const bool liveB = ring ? (bB + N <= rend && bB < a.n) : bB + N <= a.n;
                     float4 v[8];
                     {
                         float2 va[8], vb[8];
-                        load8_block32<T>(a, bA + tt, liveA, va);
-                        load8_block32<T>(a, bB + tt, liveB, vb);
+                        if (ring && ((liveA && (bA < 0 || bA + N > a.n)) || (liveB && (bB < 0 || bB + N > a.n)))) {
+                            // a block straddles the stream's ends (rare): guarded loads
+                            double2 da[8], db[8];
+                            load8_block_part<T>(a, bA + tt, da);
+                            load8_block_part<T>(a, bB + tt, db);
+#pragma unroll
+                            for (int i = 0; i < 8; ++i) {
+                                va[i] = liveA ? make_float2((float)da[i].x, (float)da[i].y) : make_float2(0.f, 0.f);
+                                vb[i] = liveB ? make_float2((float)db[i].x, (float)db[i].y) : make_float2(0.f, 0.f);
+                            }
+                        } else {
+                            load8_block32<T>(a, bA + tt, liveA, va);
+                            load8_block32<T>(a, bB + tt, liveB, vb);
+                        }
 #pragma unroll
                         for (int i = 0; i < 8; ++i) v[i] = make_float4(va[i].x, va[i].y, vb[i].x, vb[i].y);
                     }
@@ -2528,8 +2582,9 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
         }
         if (!(T <= 64 && a.t2_f32)) {
             for (long base = pos;; base += (long)G * N) {
-                if (scan_stop(base)) {
-                    stop = true;
+                if (const int ss = scan_stop(base)) {
+                    stop = ss == 1;
+                    miss = ss == 2;
                     break;
                 }
                 const int bg = t2_eval64(base);
@@ -2540,6 +2595,12 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
             }
         }
         if (stop) break;
+        if (miss) {  // rx.cpp:137-145: pos = output_size of the next buffer
+            pos = rend;
+            rend += a.ring;
+            continue;
+        }
+        if (ring && hit >= rend - a.out_len) rend += a.ring;  // rx.cpp:147-156: carry, next buffer
         const int lag = (a.tspec && !a.exact_only)
                             ? walk_preamble_fft<WT>(a, hit, big, P, tw_m, reinterpret_cast<int*>(scr + 2), xs, normv,
                                                     best, t)
@@ -2549,8 +2610,15 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
             pos = hit + a.msg;
             continue;
         }
+        if (ring && pb >= rend - a.out_len + N) rend += a.ring;  // rx.cpp:180-189
         if (pb + a.pre + a.msg > a.n) break;  // frame not in the stream: the walk ends
-        if (t == 0 && nrec < a.max_rec) a.rec[(long)c * a.max_rec + nrec] = pb;
+        if (t == 0 && nrec < a.max_rec) {
+            // ring mode: the state after the frame, (pb + msg, rend), is one of
+            // two; the record says which (a frame before the stream's first
+            // sample is kept as is: the host rejects it)
+            const bool lagr = ring && pb >= 0 && rend != ring_after(pb + a.msg);
+            a.rec[(long)c * a.max_rec + nrec] = lagr ? (pb | WALK_REC_LAG) : pb;
+        }
         if (pb >= core0 && pb < end) {  // in this chunk's core: one contiguous run of records
             if (ncore == 0) first_in = nrec;
             ++ncore;
@@ -2559,13 +2627,17 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
         // a frame of the next core located from a state before this core's
         // end: that state is the hand-over (a re-walk from pb + msg would
         // miss the frame)
-        if (past && exitp < 0) exitp = spos;
+        if (past && exitp < 0) {
+            exitp = spos;
+            exitr = srend;
+        }
         ++nrec;
         pos = pb + a.msg;  // rx.cpp:192
     }
     if (t0 == 0) {
         a.nrec[c] = nrec;
         a.exit_pos[c] = exitp;
+        if (a.exit_ring) a.exit_ring[c] = exitr;
         if (a.ncore) {
             a.ncore[c] = ncore;
             a.first_in[c] = first_in;
@@ -2720,7 +2792,7 @@ __global__ void __launch_bounds__(1024) compact_kernel(CompactArgs a)
                     lo = go && le ? mid : lo;
                     hi = go && !le ? mid : hi;
                 }
-                pbv[g] = rec[srcb[lo] + (idx - excl[lo])];
+                pbv[g] = rec[srcb[lo] + (idx - excl[lo])] & WALK_REC_PB;
             }
 #pragma unroll
             for (int g = 0; g < G; ++g) {

@@ -106,17 +106,27 @@ struct WalkArgs {
     long pre, msg;              // preamble / message lengths (samples)
     long chunk, halo;           // core samples per chunk; walk-in before the core
     long start;                 // walk state chunk 0 starts from (0: the stream's first sample)
+    // rx.cpp's SDR ring (ring > 0; ofdm_set_stream_ring): the walk state is
+    // (pos, ring end); the ring ends lie on ring_phase + k*ring. ring = 0: the
+    // continuous walk (no ring state)
+    long ring;                  // R = rx_buf_size * output_size, or 0
+    long ring_phase;            // ring ends = ring_phase + k * ring (0 <= ring_phase < ring)
+    long out_len;               // output_size (frame_len): the carry thresholds
+    long start_ring_end;        // ring end of chunk 0's start state
     long core_lo, core_hi;      // the chunk cores tile [core_lo, core_hi) (whole stream: [0, n))
     long ext;                   // walk-on past the core end while looking for the first frame there
     long ext_scan;              // >= ext: the same when the core end falls inside a T2 scan
     const int* chunk_ids;       // nullable: chunk of each workgroup (re-walk launches)
     const long* start_pos;      // nullable: exact start state per workgroup (re-walk)
+    const long* start_ring;     //   and its ring end (ring mode)
     int* queue;                 // nullable: chunk counter (zeroed) the workgroups take chunks from until
     long nchunks;               //   nchunks are taken (dynamic balance); else one chunk per workgroup
     int max_rec;                // records per chunk
-    long* rec;                  // [chunk][max_rec] preamble starts found
+    long* rec;                  // [chunk][max_rec] preamble starts found (| WALK_REC_LAG: ring mode's
+                                //   state after the frame has the later of its two possible ring ends)
     int* nrec;                  // [chunk] frames found (> max_rec: overflow)
     long* exit_pos;             // [chunk] walk state at exit; -1: stream exhausted
+    long* exit_ring;            // [chunk] its ring end (ring mode)
     int* ncore;                 // nullable: [chunk] records inside the chunk's own core (a contiguous run:
     int* first_in;              //   the walk only moves forward) and the index of the first of them
     int exact_only;             // 1: always the serial-recurrence preamble search (test hook, OFDM_WALK_EXACT=1)
@@ -127,6 +137,13 @@ struct WalkArgs {
     const double2* tspec;       // sum_j c_j e^{+2 pi i k j / M}, k < M
     double tspec_max;           // max_k |tspec_k| (error bound)
 };
+// A walk record is a preamble start, plus in ring mode the walk state after
+// the frame: (pb + message_len, ring end), where the ring end is the first
+// ring end past pb + message_len, or the one after it (the next buffer was
+// loaded by a carry, rx.cpp:147-156,180-189): bit 62 marks the second case.
+// Two walks with equal records are in equal states from there on.
+constexpr long WALK_REC_LAG = 1L << 62;
+constexpr long WALK_REC_PB = WALK_REC_LAG - 1;
 constexpr int WALK_FFT_LOGM = 9;
 constexpr int WALK_FFT_M = 1 << WALK_FFT_LOGM;
 // Samples one T2 scan step of a walker covers at most (stream_walk_kernel:

@@ -60,6 +60,11 @@ class WalkTuning(C.Structure):
                 ("exact_search", C.c_int), ("t2_f32", C.c_int), ("t2_margin", C.c_double)]
 
 
+class WalkState(C.Structure):
+    """ofdm_walk_state: (pos, ring_end) of the stream walk."""
+    _fields_ = [("pos", C.c_long), ("ring_end", C.c_long)]
+
+
 class OfdmError(RuntimeError):
     def __init__(self, code: int, msg: str):
         super().__init__(f"ofdm error {code} ({ERRORS.get(code, '?')}): {msg}")
@@ -111,8 +116,11 @@ SIGNATURES = {
     "ofdm_sync_frames": (_I, [_V, _V, _SZ, _SZ, _I, _V, _V, _V, _V]),
     "ofdm_rx_stream": (_I, [_V, _V, _SZ, _SZ, _L, _V, _V, _V, _V, C.POINTER(_SZ), _V]),
     "ofdm_rx_stream_i16": (_I, [_V, _V, _SZ, _SZ, _L, _V, _V, _V, _V, C.POINTER(_SZ), _V]),
-    "ofdm_rx_stream_shard": (_I, [_V, _V, _V, _SZ, _L, _L, _L, _SZ, _L, _V, _V, _V, _V, C.POINTER(_SZ), _V, _SZ,
-                                  C.POINTER(_SZ), C.POINTER(_L), _V]),
+    "ofdm_rx_stream_shard": (_I, [_V, _V, _V, _SZ, C.POINTER(WalkState), _L, _L, _SZ, _L, _V, _V, _V, _V,
+                                  C.POINTER(_SZ), _V, _V, _SZ, C.POINTER(_SZ), C.POINTER(WalkState), _V]),
+    "ofdm_stream_initial_state": (_I, [_V, C.POINTER(WalkState)]),
+    "ofdm_set_stream_ring": (_I, [_V, _L]),
+    "ofdm_get_stream_ring": (_I, [_V, C.POINTER(_L)]),
     "ofdm_stream_shard_margins": (_I, [_V, C.POINTER(_L), C.POINTER(_L)]),
     "ofdm_host_alloc": (_I, [_V, _SZ, C.POINTER(_V)]),
     "ofdm_host_free": (_I, [_V, _V]),
@@ -342,7 +350,8 @@ class Modem:
 
     def rx_stream(self, iq, n: int, max_frames: int, pb_out=None, bytes_out=None, constell_out=None,
                   cfo_out=None, chunk: int = 0, stream=None) -> int:
-        """rx.cpp:125-221 over a device-resident stream; returns the frames found."""
+        """rx.cpp:94-221 (with its SDR ring, ofdm_set_stream_ring) over a
+        device-resident stream; returns the frames found."""
         m = C.c_size_t()
         check(lib().ofdm_rx_stream(self.h, _ptr(iq), n, max_frames, chunk, _ptr(pb_out), _ptr(bytes_out),
                                    _ptr(constell_out), _ptr(cfo_out), C.byref(m), _stream(stream)))
@@ -376,24 +385,44 @@ class Modem:
         check(lib().ofdm_stream_shard_margins(self.h, C.byref(h), C.byref(t)))
         return h.value, t.value
 
-    def rx_stream_shard(self, iq, n: int, start: int, own_lo: int, own_hi: int, max_frames: int, pb_out=None,
+    def stream_ring(self, ring: int | None = None) -> int:
+        """ofdm_get/set_stream_ring: rx.cpp's SDR ring R of the stream walk (0:
+        the continuous walk). With `ring` set, changes it; returns the old R."""
+        old = C.c_long()
+        check(lib().ofdm_get_stream_ring(self.h, C.byref(old)))
+        if ring is not None:
+            check(lib().ofdm_set_stream_ring(self.h, ring))
+        return old.value
+
+    def initial_state(self) -> tuple[int, int]:
+        """ofdm_stream_initial_state: rx.cpp's first walk state (pos, ring_end)."""
+        st = WalkState()
+        check(lib().ofdm_stream_initial_state(self.h, C.byref(st)))
+        return st.pos, st.ring_end
+
+    def rx_stream_shard(self, iq, n: int, start, own_lo: int, own_hi: int, max_frames: int, pb_out=None,
                         bytes_out=None, constell_out=None, cfo_out=None, chunk: int = 0, i16: bool = False,
                         located_cap: int = 4096, stream=None):
-        """ofdm_rx_stream_shard: the walk from state `start` over this shard's n
-        samples, frames with pb in [own_lo, own_hi) decoded. Returns (frames
-        decoded, located pbs (numpy int64, relative), exit state)."""
+        """ofdm_rx_stream_shard: the walk from state `start` = (pos, ring_end)
+        over this shard's n samples, frames with pb in [own_lo, own_hi)
+        decoded. Returns (frames decoded, located pbs (numpy int64, relative),
+        their ring lags (numpy uint8), exit state (pos, ring_end))."""
         import numpy as np
-        m, nl, ex = C.c_size_t(), C.c_size_t(), C.c_long()
-        loc = self._located if getattr(self, "_located", None) is not None and \
-            len(self._located) >= max(1, located_cap) else np.empty(max(1, located_cap), dtype=np.int64)
-        self._located = loc
-        check(lib().ofdm_rx_stream_shard(self.h, None if i16 else _ptr(iq), _ptr(iq) if i16 else None, n, start,
-                                         own_lo, own_hi, max_frames, chunk, _ptr(pb_out), _ptr(bytes_out),
-                                         _ptr(constell_out), _ptr(cfo_out), C.byref(m), loc.ctypes.data,
-                                         located_cap, C.byref(nl), C.byref(ex), _stream(stream)))
+        m, nl, ex = C.c_size_t(), C.c_size_t(), WalkState()
+        cap = max(1, located_cap)
+        if getattr(self, "_located", None) is None or len(self._located) < cap:
+            self._located = np.empty(cap, dtype=np.int64)
+            self._located_lag = np.empty(cap, dtype=np.uint8)
+        loc, lag = self._located, self._located_lag
+        st = WalkState(*start)
+        check(lib().ofdm_rx_stream_shard(self.h, None if i16 else _ptr(iq), _ptr(iq) if i16 else None, n,
+                                         C.byref(st), own_lo, own_hi, max_frames, chunk, _ptr(pb_out),
+                                         _ptr(bytes_out), _ptr(constell_out), _ptr(cfo_out), C.byref(m),
+                                         loc.ctypes.data, lag.ctypes.data, located_cap, C.byref(nl), C.byref(ex),
+                                         _stream(stream)))
         if nl.value > located_cap:
             raise OfdmError(-1, f"located list of {nl.value} frames exceeds located_cap={located_cap}")
-        return m.value, loc[:nl.value].copy(), ex.value
+        return m.value, loc[:nl.value].copy(), lag[:nl.value].copy(), (ex.pos, ex.ring_end)
 
     def sync_frames(self, frames, nframes: int, frame_stride: int, stages: int = SYNC_ALL,
                     cfo_in=None, cfo_out=None, chan_out=None, stream=None):

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define OFDM_MI355X_ABI_VERSION 1
+#define OFDM_MI355X_ABI_VERSION 2
 
 enum {
     OFDM_OK = 0,
@@ -324,13 +324,28 @@ int ofdm_sync_frames(ofdm_ctx* ctx, double* frames, size_t nframes, size_t frame
                      int stages, const double* cfo_in, double* cfo_out, double* chan_out,
                      void* stream);
 
-/* ---- streaming rx (rx.cpp:125-221) -------------------------------------
- * Every frame the reference's detection walk finds in a contiguous stream of
- * n complex samples (device), then the main.cpp:60-80 chain and demod on each:
- *   pos = 0; hit = find_t2sin(pos); pb = find_preamble(hit) + 1;
- *   pb < -2 -> pos = hit + message_len; frame past the end -> stop;
- *   else the frame [pb, pb + preamble_len + message_len) is decoded and
- *   pos = pb + message_len.
+/* ---- streaming rx (rx.cpp:94-221) --------------------------------------
+ * Every frame rx.cpp's receive loop locates in a stream of n complex samples
+ * (device), then the main.cpp:60-80 chain and demod on each. The walk
+ * (rx.cpp:126-198) is, per step:
+ *   hit = find_t2sin(pos) (blocks pos + k*T2sin_size); pb = find_preamble(hit) + 1;
+ *   pb < -2 -> pos = hit + message_len; else the frame
+ *   [pb, pb + preamble_len + message_len) is decoded and pos = pb + message_len.
+ * rx.cpp runs it over its SDR ring (from_sdr_buf, rx.cpp:73-91,137-189): the
+ * buffer holds output_size + R samples, R = rx_buf_size * output_size (one SDR
+ * refill, sdr.hpp:141); find_t2sin only tests blocks that end inside the
+ * buffer; a T2 miss refills WITHOUT carrying the tail and restarts the grid
+ * at the new buffer, and a hit (preamble) in the buffer's last output_size
+ * (+ T2sin_size) samples carries them to the front before the refill. So a
+ * marker straddling a refill can be lost, and the grid's phase depends on
+ * the ring. The stream API reproduces this exactly (ring mode, the default
+ * when the config's rx_buf_size > 0: R from the config; ofdm_set_stream_ring
+ * changes R, 0 = no ring, the continuous walk over the stream held whole).
+ * In ring mode sample 0 of `iq` is the SDR's first sample and the walk starts
+ * as rx.cpp does, at the zero header before it (ofdm_stream_initial_state);
+ * samples past n read as zero (the walk ends once its scan passes n).
+ * A frame the walk locates past the stream end stops the walk. A frame whose
+ * preamble would start before sample 0 fails with OFDM_ERR_UNSUPPORTED.
  * The walk runs as parallel chunk walkers stitched into the one sequential
  * walk (chunk = samples per walker, 0 = automatic). Outputs (device, nullable):
  * pb_out[f] preamble start, bytes_out (bytes_per_frame per frame),
@@ -349,30 +364,50 @@ int ofdm_rx_stream_i16(ofdm_ctx* ctx, const int16_t* iq16, size_t n, size_t max_
                        long* pb_out, uint8_t* bytes_out, double* constell_out, double* cfo_out,
                        size_t* nframes_out, void* stream);
 
+/* rx.cpp's SDR ring for the stream walk: R samples per refill (>= 2 *
+ * output_size), 0 = the continuous walk. Default: rx_buf_size * output_size. */
+int ofdm_set_stream_ring(ofdm_ctx* ctx, long ring);
+int ofdm_get_stream_ring(const ofdm_ctx* ctx, long* ring);
+
+/* A state of the stream walk: the position of the next T2 search and, in
+ * ring mode, one past the last sample of the ring buffer's current SDR
+ * refill (stream coordinates; 0 without a ring). */
+typedef struct ofdm_walk_state {
+    long pos;
+    long ring_end;
+} ofdm_walk_state;
+/* rx.cpp's initial state (rx.cpp:105-114): ring mode {-output_size, R} (pos 0
+ * of a buffer whose zero header precedes the first SDR buffer), else {0, 0}. */
+int ofdm_stream_initial_state(const ofdm_ctx* ctx, ofdm_walk_state* out);
+
 /* One shard of a longer stream (multi-GPU streaming rx; the
  * reference's rx.cpp:145-156 carries one frame from ring to ring, this is the
  * same hand-over between GPUs). Exactly one of iq (complex f64) / iq16
  * (complex<int16>) is set; it holds the shard's n samples: its core plus a
  * walk-in halo before it and a tail after it. The walk starts at state
- * `start` (0 = the first sample of the whole stream, or the predecessor
- * shard's exit state; any other position gives a speculative walk that the
- * caller checks, see c-ofdm_amd/python/ofdm_stream.py) and the frames located
- * with pb in [own_lo, own_hi) are decoded into the outputs exactly as
- * ofdm_rx_stream does (pb_out relative to iq). Requires 0 <= start and
- * 0 <= own_lo <= own_hi <= n (a start past own_lo owns only frames after it:
- * the walk moves forward).
+ * `start` (shard-relative; the whole stream's initial state, or the
+ * predecessor shard's exit state, or any other state for a speculative walk
+ * that the caller checks, see c-ofdm_amd/python/ofdm_stream.py; ring mode
+ * also fixes the ring ends' phase: start->ring_end + k*R) and the frames
+ * located with pb in [own_lo, own_hi) are decoded into the outputs exactly as
+ * ofdm_rx_stream does (pb_out relative to iq). Requires 0 <= own_lo <= own_hi
+ * <= n and start->pos >= 0 (ring mode: >= -output_size, start->pos <
+ * start->ring_end <= start->pos + R + output_size).
  *   *exit_out: the walk's first state at or past own_hi (where the next
- *     shard's walk resumes; a position equivalent to it, or the state whose
- *     step located the first frame past own_hi), -1 if the samples ran out.
- *   located (host, nullable, located_cap entries) / *nlocated_out (nullable):
- *     every frame the walk located from `start` until it stopped: those before
- *     own_lo, the owned ones, and any located past own_hi.
- * ofdm_rx_stream(iq, n) is ofdm_rx_stream_shard(iq, n, 0, 0, n). */
+ *     shard's walk resumes; a state equivalent to it, or the state whose step
+ *     located the first frame past own_hi), pos -1 if the samples ran out.
+ *   located (host, nullable, located_cap entries) / located_lag (host,
+ *     nullable: ring mode's state after the frame has the later of its two
+ *     possible ring ends) / *nlocated_out (nullable): every frame the walk
+ *     located from `start` until it stopped: those before own_lo, the owned
+ *     ones, and any located past own_hi. Two walks that located the same
+ *     frame with the same lag are in the same state from there on.
+ * ofdm_rx_stream(iq, n) is ofdm_rx_stream_shard(iq, n, initial state, 0, n). */
 int ofdm_rx_stream_shard(ofdm_ctx* ctx, const double* iq, const int16_t* iq16, size_t n,
-                         long start, long own_lo, long own_hi, size_t max_frames, long chunk,
+                         const ofdm_walk_state* start, long own_lo, long own_hi, size_t max_frames, long chunk,
                          long* pb_out, uint8_t* bytes_out, double* constell_out, double* cfo_out,
-                         size_t* nframes_out, long* located, size_t located_cap,
-                         size_t* nlocated_out, long* exit_out, void* stream);
+                         size_t* nframes_out, long* located, uint8_t* located_lag, size_t located_cap,
+                         size_t* nlocated_out, ofdm_walk_state* exit_out, void* stream);
 
 /* Samples a shard of ofdm_rx_stream_shard needs around its core
  * [own_lo, own_hi): *halo_out before own_lo for the walk-in to meet the true

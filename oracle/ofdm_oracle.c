@@ -858,38 +858,231 @@ void orc_decode_frames(const ofdm_params* p, const double* x, const long* pbs, l
     }
 }
 
-/* The detection walk of rx.cpp:125-221 over one contiguous stream (the
- * ring-buffer refills of rx.cpp keep absolute positions, so over a stream
- * held whole they are the identity):
+/* The detection walk of rx.cpp:125-221 over one contiguous stream held whole,
+ * WITHOUT rx.cpp's SDR ring (the continuous walk; orc_stream_walk_ring below
+ * has the ring and is what rx.cpp does):
  *   pos = 0; loop { hit = find_t2sin(pos) (256-sample grid from pos);
  *   none -> stop; pb = find_preamble(hit) + 1 (rx.cpp:160);
  *   pb < -2 -> pos = hit + message.size (rx.cpp:162-168);
  *   frame [pb, pb + preamble + message) past the stream end -> stop;
  *   record pb; pos = pb + message.size (rx.cpp:192) }.
- * Samples past n read as zero in the preamble search. Returns the number of
- * frames (at most max) and their preamble starts. */
+ * rx.cpp's ring differs from this at its refills (rx.cpp:137-145): a T2 miss
+ * discards the ring's unscanned tail and restarts the grid on the next SDR
+ * buffer, so a marker straddling a refill can be lost. Samples past n read as
+ * zero in the preamble search. Returns the number of frames (at most max) and
+ * their preamble starts. */
 long orc_stream_walk(const ofdm_params* p, const double* x, long n, long* pb_out, long max)
 {
+    long ex, exr;
+    return orc_stream_walk_ring(p, x, n, 0, 0, 0, n, pb_out, NULL, max, &ex, &exr);
+}
+
+/* One T2 block of T2SIN_FORM::find_t2sin (Frame.hpp:164-193) at stream
+ * position b, samples outside [0, n) read as zero (rx.cpp's zero-initialised
+ * ring header, FRAME_FORM ctor Frame.cpp:221, and the SDR stand-in's zeros
+ * past a capture's end). */
+static double t2_block_rel_at(int size, const double* mask, const cplx* x, long n, long b, cplx* blk, cplx* tmp)
+{
+    for (int i = 0; i < size; i++) blk[i] = sample_or_zero(x, n, b + i);
+    return t2_block_rel(size, mask, blk, tmp);
+}
+
+/* rx.cpp's detection walk in stream coordinates, with its SDR ring (ring > 0)
+ * or without it (ring = 0, the continuous walk).
+ *
+ * rx.cpp's ring (rx.cpp:94-198, buf_update :73-91): from_sdr_buf holds
+ * output_size + R samples, R = rx_buf_size * output_size (the SDR's
+ * rx_buf_size, sdr.hpp:141; output_size = frame_len, Frame.cpp:221-224); each
+ * refill copies the next R SDR samples to offset output_size. In stream
+ * coordinates (sample 0 = the SDR's first sample) the walk state is
+ * (pos, ring_end), ring_end = one past the ring's last sample:
+ *   start (-output_size, R): the zero header before the first buffer (:105-114);
+ *   T2 search from pos over the blocks that end by ring_end (find_t2sin's
+ *     cycles = (size - pos)/T2sin_size on the buffer, Frame.hpp:152);
+ *   a miss -> (ring_end, ring_end + R): the refill without carry, grid
+ *     restarted at output_size (:137-145);
+ *   hit >= ring_end - output_size -> ring_end += R: the carry at
+ *     pos >= threshold (:147-156);
+ *   pb = find_preamble(hit) + 1; pb < -2 -> pos = hit + message.size (:160-166);
+ *   pb >= ring_end - output_size + T2sin_size -> ring_end += R (:180-189);
+ *   record pb; pos = pb + message.size (:198).
+ * Every sample a step reads lies in the buffer, so the decoded frames are the
+ * stream's samples (orc_rx_app_walk replays the buffer itself; the tests
+ * check the two agree). Samples outside [0, n) read as zero; the walk stops
+ * when a scan starts at or past n (ring = 0: when no full block is left) or
+ * a located frame runs past n.
+ *
+ * The walk starts at (start, ring_end) (ring_end ignored when ring = 0) and
+ * stops at its first state at or past own_hi (own_hi = n: the whole stream):
+ * *exit_out / *exit_ring_out = that state (a position after a step; the
+ * first scan block at or past own_hi when the scan passes it, an equivalent
+ * state; the start of the step that located the first frame past own_hi),
+ * or -1 when the walk ended first. lag_out (nullable): per frame, whether
+ * the state after it has the later of its two possible ring ends (a carry
+ * loaded the next buffer; the library's WALK_REC_LAG). Returns the frames
+ * located (at most max stored). */
+/* The first ring end after q on the grid of ring end e (ring ends e + k*ring). */
+static long ring_after(long q, long e, long ring)
+{
+    const long d = q - e;
+    const long k = d >= 0 ? d / ring : -((-d + ring - 1) / ring);
+    return e + (k + 1) * ring;
+}
+
+long orc_stream_walk_ring(const ofdm_params* p, const double* xd, long n, long ring, long start, long ring_end,
+                          long own_hi, long* pb_out, uint8_t* lag_out, long max, long* exit_out, long* exit_ring_out)
+{
     int N = (int)p->fft_size, cp = (int)p->cp_size, L = N + cp;
-    long pre = (long)L * p->num_pr_symb, msg = (long)L * p->num_symb;
+    const int size = (int)p->t2sin_size;
+    const long pre = (long)L * p->num_pr_symb, msg = (long)L * p->num_symb, out = size + pre + msg;
+    const double level = (double)p->t2_sin_level / 1000;
+    const cplx* x = (const cplx*)xd;
     int D = (int)p->num_data_subc;
     cplx* opre = (cplx*)malloc(sizeof(cplx) * pre);
     cplx* modp = (cplx*)malloc(sizeof(cplx) * (long)D * p->num_pr_symb);
     cplx* templ = (cplx*)malloc(sizeof(cplx) * p->pr_sin_len);
+    double* mask = (double*)malloc(sizeof(double) * size);
+    cplx* blk = (cplx*)malloc(sizeof(cplx) * size);
+    cplx* tmp = (cplx*)malloc(sizeof(cplx) * size);
     orc_preamble_setup(p, (double*)opre, (double*)modp, (double*)templ);
-    long pos = 0, nf = 0;
-    while (nf < max) {
-        long hit = orc_find_t2sin(p, x, n, pos);
-        if (hit < 0) break;
-        long pb = orc_find_preamble(p, (const double*)templ, x, n, hit) + 1;
+    orc_t2_mask(p, mask);
+    long pos = start, rend = ring_end, nf = 0;
+    *exit_out = -1;
+    *exit_ring_out = 0;
+    for (;;) {
+        if (pos >= own_hi) {
+            *exit_out = pos;
+            *exit_ring_out = rend;
+            break;
+        }
+        const long spos = pos, srend = rend;
+        long hit = -1;
+        int stop = 0, miss = 0, passed = 0;
+        for (long b = pos;; b += size) {
+            if (ring ? b >= n : b + size > n) {
+                stop = 1;
+                break;
+            }
+            if (b >= own_hi) {  /* the scan passes own_hi: an equivalent state */
+                *exit_out = b;
+                *exit_ring_out = rend;
+                passed = 1;
+                break;
+            }
+            if (ring && b + size > rend) {
+                miss = 1;
+                break;
+            }
+            if (t2_block_rel_at(size, mask, x, n, b, blk, tmp) > level) {
+                hit = b;
+                break;
+            }
+        }
+        if (stop || passed) break;
+        if (miss) {
+            pos = rend;
+            rend += ring;
+            continue;
+        }
+        if (ring && hit >= rend - out) rend += ring;
+        const long pb = orc_find_preamble(p, (const double*)templ, xd, n, hit) + 1;
         if (pb < -2) {
             pos = hit + msg;
             continue;
         }
+        if (ring && pb >= rend - out + size) rend += ring;
         if (pb + pre + msg > n) break;
-        pb_out[nf++] = pb;
+        if (nf < max) {
+            pb_out[nf] = pb;
+            /* the state after the frame is (pb + msg, rend): rend is the first
+             * ring end after pb + msg, or (after a carry) the one after it */
+            if (lag_out) lag_out[nf] = ring && rend != ring_after(pb + msg, rend, ring);
+        }
+        nf++;
+        if (pb >= own_hi) {
+            *exit_out = spos;
+            *exit_ring_out = srend;
+            break;
+        }
         pos = pb + msg;
     }
+    free(tmp);
+    free(blk);
+    free(mask);
+    free(templ);
+    free(modp);
+    free(opre);
+    return nf;
+}
+
+/* rx.cpp's receive loop itself (rx.cpp:94-198 with buf_update :73-91), replayed
+ * on a real ring buffer: from_sdr_buf = output_size + R samples (Frame.cpp:221,
+ * R = rx_buf_size * output_size, sdr.hpp:141), each SDR refill written at
+ * offset output_size, the carry copying the last output_size samples to the
+ * front (:149-153, :182-186), the refill on a T2 miss leaving the front as
+ * it was. x is the SDR's sample stream (zeros past n, as the stand-in
+ * delivers). `iterations` loop iterations are run (config["iterations"],
+ * :124-126); iterations <= 0 runs until a refill's buffer starts at or past
+ * n. stop_at_end: stop at the first located frame running past n (the
+ * stream API's rule) instead of decoding the zeros after it. Frames are
+ * reported as stream positions (buffer index + the buffer's stream offset). */
+long orc_rx_app_walk(const ofdm_params* p, const double* xd, long n, long iterations, int stop_at_end, long* pb_out,
+                     long max)
+{
+    int N = (int)p->fft_size, cp = (int)p->cp_size, L = N + cp;
+    const int size = (int)p->t2sin_size;
+    const long pre = (long)L * p->num_pr_symb, msg = (long)L * p->num_symb, out = size + pre + msg;
+    const long R = p->rx_buf_size * out, bufsize = out + R, threshold = bufsize - out;
+    const cplx* x = (const cplx*)xd;
+    int D = (int)p->num_data_subc;
+    cplx* opre = (cplx*)malloc(sizeof(cplx) * pre);
+    cplx* modp = (cplx*)malloc(sizeof(cplx) * (long)D * p->num_pr_symb);
+    cplx* templ = (cplx*)malloc(sizeof(cplx) * p->pr_sin_len);
+    cplx* buf = (cplx*)calloc((size_t)bufsize, sizeof(cplx));
+    orc_preamble_setup(p, (double*)opre, (double*)modp, (double*)templ);
+    long src = 0, base = 0, nf = 0;
+    /* buf_update: the next SDR buffer to offset output_size; buf[0] is then
+     * stream sample src - R - out */
+#define RING_REFILL()                                                   \
+    do {                                                                \
+        for (long i = 0; i < R; i++) buf[out + i] = sample_or_zero(x, n, src + i); \
+        src += R;                                                       \
+        base = src - R - out;                                           \
+    } while (0)
+    RING_REFILL();
+    long pos = 0;
+    for (long it = 0; iterations <= 0 || it < iterations; it++) {
+        pos = orc_find_t2sin(p, (const double*)buf, bufsize, pos);
+        if (pos == -1) {
+            pos = out;
+            if (iterations <= 0 && src >= n) break; /* the next buffer would start past the capture */
+            RING_REFILL();
+            continue;
+        }
+        if (pos >= threshold) {
+            pos -= threshold;
+            memmove(buf, buf + threshold, sizeof(cplx) * out);
+            RING_REFILL();
+        }
+        long preamble_begin = orc_find_preamble(p, (const double*)templ, (const double*)buf, bufsize, pos) + 1;
+        if (preamble_begin < -2) {
+            pos += msg;
+            continue;
+        }
+        pos = preamble_begin;
+        if (pos >= threshold + size) {
+            pos -= threshold;
+            memmove(buf, buf + threshold, sizeof(cplx) * out);
+            RING_REFILL();
+        }
+        const long pb = base + pos;
+        if (stop_at_end && pb + pre + msg > n) break;
+        if (nf < max) pb_out[nf] = pb;
+        nf++;
+        pos += msg;
+    }
+#undef RING_REFILL
+    free(buf);
     free(templ);
     free(modp);
     free(opre);

@@ -91,6 +91,11 @@ double orc_decode_frame(const ofdm_params* p, const double* region, double* cons
 void orc_decode_frames(const ofdm_params* p, const double* x, const long* pbs, long nframes, double* cfo,
                        double* constell, uint8_t* bytes, int threads);
 long orc_stream_walk(const ofdm_params* p, const double* x, long n, long* pb_out, long max);
+long orc_stream_walk_ring(const ofdm_params* p, const double* x, long n, long ring, long start, long ring_end,
+                          long own_hi, long* pb_out, uint8_t* lag_out, long max, long* exit_out,
+                          long* exit_ring_out);
+long orc_rx_app_walk(const ofdm_params* p, const double* x, long n, long iterations, int stop_at_end, long* pb_out,
+                     long max);
 
 #ifdef __cplusplus
 }

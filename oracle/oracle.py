@@ -104,6 +104,9 @@ def lib():
             "orc_decode_frame": (d, [PP, P_d, P_d, P_u8]),
             "orc_decode_frames": (v, [PP, P_d, C.POINTER(C.c_long), l, P_d, P_d, P_u8, i]),
             "orc_stream_walk": (l, [PP, P_d, l, C.POINTER(C.c_long), l]),
+            "orc_stream_walk_ring": (l, [PP, P_d, l, l, l, l, l, C.POINTER(C.c_long), P_u8, l,
+                                         C.POINTER(C.c_long), C.POINTER(C.c_long)]),
+            "orc_rx_app_walk": (l, [PP, P_d, l, l, i, C.POINTER(C.c_long), l]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -403,3 +406,54 @@ def stream_walk(params, x: np.ndarray, max_frames: int = 1 << 20) -> np.ndarray:
     out = np.zeros(max_frames, np.int64)
     nf = lib().orc_stream_walk(C.byref(p), _d(x), len(x), out.ctypes.data_as(C.POINTER(C.c_long)), max_frames)
     return out[:nf].copy()
+
+
+def ring_len(params) -> int:
+    """rx.cpp's SDR refill size R = rx_buf_size * output_size (sdr.hpp:141,
+    rx.cpp:53): 0 when rx_buf_size is 0 (no ring: the continuous walk)."""
+    p = P(params)
+    return p.rx_buf_size * geometry(p)["frame_len"]
+
+
+def stream_walk_ring(params, x: np.ndarray, ring: int | None = None, start: int | None = None,
+                     ring_end: int | None = None, own_hi: int | None = None, max_frames: int = 1 << 20,
+                     with_lags: bool = False):
+    """rx.cpp's detection walk WITH its SDR ring, in stream coordinates
+    (orc_stream_walk_ring): ring = R (None: the config's; 0: the continuous
+    walk), start state (start, ring_end) (None: rx.cpp's initial state
+    (-output_size, R)), stop at the first state at or past own_hi (None: the
+    stream end). Returns (pbs, (exit_pos, exit_ring_end)), or (pbs, lags,
+    exit) with_lags."""
+    p = P(params)
+    R = ring_len(p) if ring is None else ring
+    out_len = geometry(p)["frame_len"]
+    if start is None:
+        start = -out_len if R else 0
+    if ring_end is None:
+        ring_end = R
+    x = np.ascontiguousarray(x, np.complex128)
+    n = len(x)
+    out = np.zeros(max_frames, np.int64)
+    lag = np.zeros(max_frames, np.uint8)
+    ex, exr = C.c_long(), C.c_long()
+    nf = lib().orc_stream_walk_ring(C.byref(p), _d(x), n, R, start, ring_end, n if own_hi is None else own_hi,
+                                    out.ctypes.data_as(C.POINTER(C.c_long)), _u8(lag), max_frames, C.byref(ex),
+                                    C.byref(exr))
+    m = min(nf, max_frames)
+    if with_lags:
+        return out[:m].copy(), lag[:m].copy(), (ex.value, exr.value)
+    return out[:m].copy(), (ex.value, exr.value)
+
+
+def rx_app_walk(params, x: np.ndarray, iterations: int = 0, stop_at_end: bool = True,
+                max_frames: int = 1 << 20) -> np.ndarray:
+    """rx.cpp:94-198 replayed on a real ring buffer (orc_rx_app_walk): the
+    frames its loop locates in `iterations` iterations (0: until the capture
+    is used up) from the SDR stream x (zeros past its end), as stream
+    positions."""
+    p = P(params)
+    x = np.ascontiguousarray(x, np.complex128)
+    out = np.zeros(max_frames, np.int64)
+    nf = lib().orc_rx_app_walk(C.byref(p), _d(x), len(x), iterations, int(stop_at_end),
+                               out.ctypes.data_as(C.POINTER(C.c_long)), max_frames)
+    return out[:min(nf, max_frames)].copy()

@@ -202,17 +202,21 @@ def test_compat_device_mirrors_equal_staged_path(tmp_path, name):
 def test_reference_tx_rx_apps_stream_120_frames(tmp_path):
     """The reference's own tx.cpp frames a 120-frame payload file into the SDR
     stand-in's int16 capture (data/tx.bin layout); its own rx.cpp streams the
-    capture (with 0-3000-sample silences between the bursts) through the ring
-    buffer, the detection walk and the per-frame sync chain on the
+    capture (with 0-3000-sample silences between the bursts) through its
+    ring buffer, the detection walk and the per-frame sync chain on the
     device-mirrored FRAME_FORM, and writes every payload it decodes to
-    Res.wav. Every written payload equals a sent one, in order, and rx.cpp's
-    walk locates at least 90% of the frames (its T2 search tests blocks on a
-    256-sample grid, Frame.hpp:164, so a frame whose marker straddles two grid
-    blocks can be missed, as in the reference)."""
+    Res.wav. The written payloads must be exactly, in order, those of the
+    frames rx.cpp's loop locates when replayed by the oracle on a real ring
+    buffer (orc_rx_app_walk: the zero header, 40-frame refills, the refill
+    without carry on a T2 miss, the carries, the iteration cap), each decoded
+    by the oracle's main.cpp:60-80 chain; and the stream API in ring mode
+    locates the same frames."""
     nfr = 120
-    write_config(tmp_path, D, iterations=nfr + 60)
+    iters = nfr + 60
+    write_config(tmp_path, D, iterations=iters)
     g = O.geometry(D)
     pay = g["bytes_per_frame"] - 8
+    # per-frame distinct payloads (frame f's bytes shift by 249 f mod 256: 256 distinct frames)
     body = bytes((i * 131 + 7 + (i // pay) * 17) & 0xFF for i in range(nfr * pay))
     (tmp_path / "FlyMeToTheMoon_mono.wav").write_bytes(body)
     txf = tmp_path / "tx.bin"
@@ -223,10 +227,28 @@ def test_reference_tx_rx_apps_stream_120_frames(tmp_path):
     r = run([os.path.join(REF_BIN, "rx")], tmp_path, {"OFDM_SDR_RX_FILE": str(txf)}, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     res = (tmp_path / "Res.wav").read_bytes()
-    chunks = [body[i * pay:(i + 1) * pay] for i in range(nfr)]
-    got = [res[i * pay:(i + 1) * pay] for i in range(len(res) // pay)]
     assert len(res) % pay == 0
+    got = [res[i * pay:(i + 1) * pay] for i in range(len(res) // pay)]
+    chunks = [body[i * pay:(i + 1) * pay] for i in range(nfr)]
+    # the oracle's replay of rx.cpp's loop over the same SDR samples
+    w = np.fromfile(txf, np.int16).astype(np.float64)
+    x = w[0::2] + 1j * w[1::2]
+    pbs = O.rx_app_walk(D, x, iterations=iters, stop_at_end=False)
+    span = g["preamble_len"] + g["message_len"]
+    xz = np.concatenate([x, np.zeros(span, np.complex128)])  # the stand-in's zeros past the capture
+    want = [O.decode_frame(D, xz[pb:pb + span])[2][8:].tobytes() for pb in pbs]
+    assert len(got) == len(want), f"rx wrote {len(got)} payloads, its loop locates {len(want)} frames"
+    assert got == want
     idx = [chunks.index(c) if c in chunks else -1 for c in got]
-    assert -1 not in idx, f"{idx.count(-1)} of {len(got)} written payloads match no sent frame"
-    assert idx == sorted(idx) and len(set(idx)) == len(idx)
-    assert len(got) >= 0.9 * nfr, f"only {len(got)} of {nfr} frames decoded"
+    assert -1 not in idx and idx == sorted(idx) and len(set(idx)) == len(idx)
+    assert len(got) >= 0.9 * nfr
+    # the stream API (ring mode, the config's R) locates the same frames
+    import torch
+    import ofdm_mi355x as M
+    m = M.Modem(D, 0)
+    inside = [pb for pb in pbs if pb + span <= len(x)]
+    pb_out = torch.full((nfr + 8,), -1, dtype=torch.int64, device="cuda")
+    nf = m.rx_stream(torch.from_numpy(x).cuda(), len(x), nfr + 8, pb_out=pb_out)
+    torch.cuda.synchronize()
+    assert nf == len(inside) and list(pb_out[:nf].cpu().numpy()) == inside
+    m.close()

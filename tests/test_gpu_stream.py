@@ -1,8 +1,11 @@
-"""GPU parity of the streaming receiver (rx.cpp:125-221):
-ofdm_rx_stream's chunk-parallel walk must locate exactly the frames of the
-sequential walk (oracle orc_stream_walk) and decode each as main.cpp:60-80
-(oracle orc_decode_frame) — on the reference capture data/data.bin and on
-synthetic impaired streams, for any chunking of the walk."""
+"""GPU parity of the streaming receiver (rx.cpp:94-221):
+ofdm_rx_stream's chunk-parallel walk must locate exactly the frames of
+rx.cpp's sequential walk over its SDR ring (oracle orc_stream_walk_ring,
+itself pinned to rx.cpp's loop replayed on a real ring buffer in
+tests/test_stream_shard.py), or of the continuous walk with the ring off
+(orc_stream_walk), and decode each as main.cpp:60-80 (oracle
+orc_decode_frame) — on the reference capture data/data.bin and on synthetic
+impaired streams, for any chunking of the walk and any ring size."""
 import ctypes as C
 
 import numpy as np
@@ -38,14 +41,20 @@ def host(t):
 GD = golden()
 
 
-def run_stream(cfg, x, max_frames=4096, chunk=0, tuning=None):
+def run_stream(cfg, x, max_frames=4096, chunk=0, tuning=None, ring=None):
     m = modem(cfg)
     if tuning:
         old = m.walk_tuning(**tuning)
         try:
-            return run_stream(cfg, x, max_frames, chunk)
+            return run_stream(cfg, x, max_frames, chunk, ring=ring)
         finally:
             m.walk_tuning(**old)
+    if ring is not None:
+        old = m.stream_ring(ring)
+        try:
+            return run_stream(cfg, x, max_frames, chunk)
+        finally:
+            m.stream_ring(old)
     g = O.geometry(cfg)
     dx = dev(x)
     pbs = torch.full((max_frames,), -1, dtype=torch.int64, device="cuda")
@@ -60,9 +69,15 @@ def run_stream(cfg, x, max_frames=4096, chunk=0, tuning=None):
             host(cfo)[:k])
 
 
-def check_against_oracle(cfg, x, got):
+def want_walk(cfg, x, ring=None):
+    """The oracle's walk: rx.cpp's ring (ring None: the config's R), or the
+    continuous walk (ring 0)."""
+    return O.stream_walk_ring(cfg, x, ring=ring)[0]
+
+
+def check_against_oracle(cfg, x, got, ring=None):
     nf, pbs, out, cons, cfo = got
-    want = O.stream_walk(cfg, x)
+    want = want_walk(cfg, x, ring)
     assert nf == len(want)
     assert np.array_equal(pbs, want)
     g = O.geometry(cfg)
@@ -88,6 +103,51 @@ def test_stream_config4_matches_sequential_walk(chunk):
     x, data = impaired_stream(D, 40, seed=4)
     want = check_against_oracle(D, x, run_stream(D, x, chunk=chunk))
     assert len(want) >= 20  # the grid-relative T2 search misses some frames, as the reference does
+
+
+def test_stream_continuous_walk_matches_oracle():
+    # ring 0: the continuous walk over the stream held whole (orc_stream_walk)
+    x, data = impaired_stream(D, 40, seed=4)
+    for chunk in (0, 9000):
+        got = run_stream(D, x, chunk=chunk, ring=0)
+        want = check_against_oracle(D, x, got, ring=0)
+        assert np.array_equal(want, O.stream_walk(D, x))
+
+
+# rx.cpp's ring with 2- and 3-frame refills: a ring end every ~2 frames of the
+# stream, so most steps meet a refill (misses that restart the grid, carries)
+RING_CFGS = [dict(D, rx_buf_size=2), dict(D, rx_buf_size=3)]
+
+
+@pytest.mark.parametrize("rcfg", RING_CFGS, ids=["rb2", "rb3"])
+@pytest.mark.parametrize("chunk", [0, 5000, 9000, 20000])
+def test_stream_ring_walk_matches_rx_cpp_loop(rcfg, chunk):
+    x, data = impaired_stream(rcfg, 40, seed=4)
+    want = check_against_oracle(rcfg, x, run_stream(rcfg, x, chunk=chunk))
+    assert np.array_equal(want, O.rx_app_walk(rcfg, x))  # rx.cpp's loop on a real ring buffer
+    assert not np.array_equal(want, O.stream_walk(rcfg, x))  # the ring loses frames here
+
+
+@pytest.mark.parametrize("halo,ext", [(0, 0), (250, 0), (100, 2000)])
+@pytest.mark.parametrize("chunk", [5000, 20000])
+def test_stream_ring_short_halo_rewalks(halo, ext, chunk):
+    # re-walks from ring states (position and ring end) stay exact
+    rcfg = RING_CFGS[1]
+    x, data = impaired_stream(rcfg, 40, seed=6, gap_max=6000)
+    check_against_oracle(rcfg, x, run_stream(rcfg, x, chunk=chunk, tuning=dict(halo_milli=halo, ext_milli=ext)))
+
+
+def test_stream_ring_validation_and_state():
+    m = modem(D)
+    g = O.geometry(D)
+    assert m.stream_ring() == 40 * g["frame_len"] == O.ring_len(D)  # rx_buf_size * output_size
+    assert m.initial_state() == (-g["frame_len"], 40 * g["frame_len"])
+    for bad in (-1, g["frame_len"]):
+        with pytest.raises(M.OfdmError):
+            m.stream_ring(bad)
+    old = m.stream_ring(0)
+    assert m.initial_state() == (0, 0)
+    m.stream_ring(old)
 
 
 @pytest.mark.parametrize("halo,ext", [(0, 0), (100, 0), (250, 0), (500, 0), (100, 2000), (1500, 2000)])
@@ -185,13 +245,24 @@ def test_stream_edges():
     assert run_stream(D, noise[:100])[0] == 0
     # max_frames truncates outputs but reports every frame found
     x, _ = impaired_stream(D, 10, seed=21)
-    want = O.stream_walk(D, x)
+    want = want_walk(D, x)
     nf, pbs, out, _, _ = run_stream(D, x, max_frames=3)
     assert nf == len(want) and np.array_equal(pbs, want[:3])
     # a stream cut inside the last frame drops it, as the walk stops there
     cut = want[-1] + g["preamble_len"] + g["message_len"] - 1
     nf2, pbs2, *_ = run_stream(D, x[:cut])
-    assert np.array_equal(pbs2, O.stream_walk(D, x[:cut])) and nf2 == len(want) - 1
+    assert np.array_equal(pbs2, want_walk(D, x[:cut])) and nf2 == len(want) - 1
+    # ring mode: a capture that starts inside a frame's preamble would have
+    # rx.cpp decode from its zero header; the stream API reports it (or, if
+    # the walk does not lock there, simply starts later), never reads before 0
+    for cut0 in (g["frame_len"] // 2, 300, 40, 0):
+        y = x[max(0, want[0] - cut0):]
+        w = want_walk(D, y)
+        if len(w) and w[0] < 0:
+            with pytest.raises(M.OfdmError, match="before the stream"):
+                run_stream(D, y)
+        else:
+            assert np.array_equal(run_stream(D, y)[1], w)
 
 
 def to_i16(x):

@@ -1,11 +1,17 @@
 """GPU parity of the streaming receiver at the config-4 bench size (SURVEY §8d
 config 4; tools/stream_bench.py's stream: 16 384 D-config frames, 0-4096
 gaps, CFO +-0.004, random phase, 20 dB AWGN; 132 M samples). The GPU's
-chunk-parallel walk must equal the oracle's sequential rx.cpp:125-221 walk
-over the whole stream, and every located frame must decode as the oracle's
-main.cpp:60-80 chain does (CFO exact, constellation to 1e-9, bytes exact
-outside the rounding band of a threshold). The oracle walk and the OpenMP
-decode of all ~16 000 frames take a few seconds of CPU."""
+chunk-parallel walk must equal the oracle's sequential rx.cpp:94-198 walk
+over the whole stream, with rx.cpp's SDR ring (the default; the oracle's ring
+walk is checked against rx.cpp's loop replayed on a real ring buffer here
+too) and without it, and every located frame must decode as the oracle's
+main.cpp:60-80 chain does (CFO exact, constellation to 1e-9, every decision
+equal). The per-run summaries go to gpurun_out/stream_full_summary.jsonl.
+The oracle walk and the OpenMP decode of all ~16 000 frames take a few
+seconds of CPU."""
+import json
+import os
+
 import numpy as np
 import pytest
 
@@ -58,16 +64,19 @@ def run_full(m, x, n, nf, i16):
             cons.cpu().numpy().reshape(nf, -1)[:k], cfo.cpu().numpy()[:k])
 
 
-@pytest.mark.parametrize("i16", [False, True], ids=["f64", "int16"])
-def test_stream_bench_size_every_frame_matches_oracle(i16):
+@pytest.mark.parametrize("i16,ring", [(False, True), (True, True), (False, False)],
+                         ids=["f64", "int16", "f64-continuous"])
+def test_stream_bench_size_every_frame_matches_oracle(i16, ring):
     """The config-4 bench stream (16 384 frames, 132 M samples), f64 and the
     int16 wire format: the walk equals the oracle's sequential walk, and EVERY
     located frame decodes as the oracle's main.cpp:60-80 chain on the same
-    samples (CFO exact, constellation 1e-9, bytes equal outside the rounding
-    band of a threshold; see common.check_stream_frames)."""
+    samples (CFO exact, constellation 1e-9, every decision equal; see
+    common.check_stream_frames)."""
     cfg = dict(O.DEFAULT)
     nf = 16384
     m, x, n = build_stream(cfg, nf, seed=5 if i16 else 4)
+    if not ring:
+        m.stream_ring(0)
     if i16:
         # the SDR wire format: the GPU reads complex<int16>, the oracle their exact doubles
         x16 = (torch.view_as_real(x) * float(cfg["mult"])).round().clamp(-32768, 32767).to(torch.int16).reshape(-1)
@@ -78,10 +87,18 @@ def test_stream_bench_size_every_frame_matches_oracle(i16):
     else:
         h = x.cpu().numpy()
         found, pbs, out, cons, cfo = run_full(m, x, n, nf, False)
-    want = O.stream_walk(cfg, h)
+    if ring:
+        want = O.stream_walk_ring(cfg, h)[0]
+        assert np.array_equal(want, O.rx_app_walk(cfg, h))  # rx.cpp's loop on a real ring buffer
+    else:
+        want = O.stream_walk(cfg, h)
     assert found == len(want) and found > 0.95 * nf
     assert np.array_equal(pbs, want[:len(pbs)])
     summary = check_stream_frames(cfg, h, pbs, out, cons, cfo)
-    assert summary["frames"] == found
-    print(f"{'int16' if i16 else 'f64'} stream: {summary}")
+    assert summary["frames"] == found and summary["decision_flips"] == 0
+    summary.update(stream="int16" if i16 else "f64", ring=int(m.stream_ring()), samples=int(n),
+                   frames_sent=nf)
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(os.path.join("gpurun_out", "stream_full_summary.jsonl"), "a") as f:
+        f.write(json.dumps(summary) + "\n")
     m.close()

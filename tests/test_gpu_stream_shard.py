@@ -3,8 +3,8 @@ ofdm_rx_stream_shard): the stream is split into 2..8 sample shards, each with
 its walk-in halo and tail, each run on its OWN ofdm_ctx (as one rank per GPU
 would run it; here all on the box's one MI355X), with the report / plan /
 re-walk protocol between them (ofdm_stream.run_local). The union of the owned
-frames must equal the oracle's one sequential rx.cpp:125-221 walk over the
-whole stream (indices exact), and the owned frames decode as the oracle's
+frames must equal the oracle's one sequential rx.cpp:94-198 walk with its SDR
+ring over the whole stream (indices exact; orc_stream_walk_ring), and the owned frames decode as the oracle's
 main.cpp:60-80 chain (CFO exact, bytes exact, constellation to 1e-9); at the
 bench size (config 4, 132 M samples) too."""
 import numpy as np
@@ -28,8 +28,8 @@ def run_sharded(cfg, x, n, world, halo=None, i16=False, max_frames=None):
     g = O.geometry(cfg)
     rxs, walks, outs, mods = [], [], [], []
     for r in range(world):
-        rx = SS.ShardedStreamRx(cfg, n, world, r, halo=halo)
         m = M.Modem(cfg, 0)
+        rx = SS.ShardedStreamRx(cfg, n, world, r, halo=halo, ring=m.stream_ring(), initial=m.initial_state())
         xs = x[2 * rx.slice_lo:2 * rx.slice_hi] if i16 else x[rx.slice_lo:rx.slice_hi]
         cap = max_frames or (rx.slice_hi - rx.slice_lo) // g["message_len"] + 8
         o = {"pb_out": torch.full((cap,), -1, dtype=torch.int64, device="cuda"),
@@ -70,8 +70,8 @@ def check_frames(cfg, h, want, got, pick=None):
 
 @pytest.fixture(scope="module")
 def small():
-    x, _ = impaired_stream(D, 40, seed=4)
-    return x, O.stream_walk(D, x)
+    x, _ = impaired_stream(D, 90, seed=4)  # ~3 ring ends of the config's 40-frame ring
+    return x, O.stream_walk_ring(D, x)[0]
 
 
 @pytest.mark.parametrize("world", [2, 3, 5, 8])
@@ -95,14 +95,27 @@ def test_sharded_stream_int16_equals_f64(small):
     x16 = O.get_int16(x, D["mult"]).reshape(-1)
     h = x16.reshape(-1, 2).astype(np.float64)
     h = h[:, 0] + 1j * h[:, 1]
-    want = O.stream_walk(D, h)
+    want = O.stream_walk_ring(D, h)[0]
     got = run_sharded(D, torch.from_numpy(np.ascontiguousarray(x16)).cuda(), len(x), 3, i16=True)
     check_frames(D, h, want, got)
 
 
+RB3 = dict(D, rx_buf_size=3)
+
+
+@pytest.mark.parametrize("world,halo", [(3, None), (5, 0), (4, 2500)])
+def test_sharded_stream_small_ring(world, halo):
+    # a ring end every ~2.4 frames: shards start speculatively in ring
+    # states, exit states carry the ring end, re-walks resume from them
+    x, _ = impaired_stream(RB3, 40, seed=4)
+    want = O.stream_walk_ring(RB3, x)[0]
+    got = run_sharded(RB3, torch.from_numpy(x).cuda(), len(x), world, halo=halo)
+    check_frames(RB3, x, want, got)
+
+
 def test_sharded_stream_more_shards_than_frames():
     x, _ = impaired_stream(D, 3, seed=11)
-    want = O.stream_walk(D, x)
+    want = O.stream_walk_ring(D, x)[0]
     got = run_sharded(D, torch.from_numpy(x).cuda(), len(x), 8)
     check_frames(D, x, want, got)
 
@@ -136,5 +149,5 @@ def _bench_walk(h):
     key = (len(h), float(h[12345].real))
     if key not in _WALK:
         _WALK.clear()
-        _WALK[key] = O.stream_walk(dict(O.DEFAULT), h)
+        _WALK[key] = O.stream_walk_ring(dict(O.DEFAULT), h)[0]
     return _WALK[key]

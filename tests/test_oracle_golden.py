@@ -94,6 +94,10 @@ def test_stream_walk_and_decode_match_reference_capture():
     # a stream cut inside frame 2 yields frame 1 only; before frame 1's end, none
     assert list(O.stream_walk(G, GD["data"][: pbs[1] + span - 1])) == [pbs[0]]
     assert list(O.stream_walk(G, GD["data"][: pbs[0] + span - 1])) == []
+    # rx.cpp's own loop over data.bin as its SDR stream (ring buffer, zero
+    # header, 40-frame refills) and the ring walk's state form find the same two
+    assert list(O.rx_app_walk(G, GD["data"])) == list(GD["preamble_begin"])
+    assert list(O.stream_walk_ring(G, GD["data"])[0]) == list(GD["preamble_begin"])
 
 
 def test_awgn_is_counter_based_and_thread_independent():

@@ -72,7 +72,8 @@ def main():
     with tempfile.TemporaryDirectory() as d:
         write_config(d, D, iterations=args.frames + 40)
         pay = g["bytes_per_frame"] - 8
-        body = bytes((i * 131 + 7) & 0xFF for i in range(args.frames * pay))
+        # per-frame distinct payloads (frame f's bytes shift by 249 f mod 256)
+        body = bytes((i * 131 + 7 + (i // pay) * 17) & 0xFF for i in range(args.frames * pay))
         with open(os.path.join(d, "FlyMeToTheMoon_mono.wav"), "wb") as f:
             f.write(body)
         txf = os.path.join(d, "tx.bin")
@@ -95,11 +96,15 @@ def main():
         with open(os.path.join(d, "Res.wav"), "rb") as f:
             res = f.read()
     chunks = {body[i * pay:(i + 1) * pay] for i in range(args.frames)}
+    index = {body[i * pay:(i + 1) * pay]: i for i in range(args.frames)}
+    idx = [index.get(res[i * pay:(i + 1) * pay], -1) for i in range(len(res) // pay)]
+    order_ok = -1 not in idx and idx == sorted(idx) and len(set(idx)) == len(idx)
     out = {"frames_sent": args.frames, "what": "rx.cpp per-frame iteration time (LOG.txt TIME of iterations that decoded a frame without a "
                    "ring refill), reference rx.cpp compiled unchanged on the drop-in layer",
            "config": "D (config/config.txt)", "frames_decoded": len(ours),
            "frames_written": len(res) // pay,
            "frames_payload_exact": sum(res[i * pay:(i + 1) * pay] in chunks for i in range(len(res) // pay)),
+           "frames_in_order": order_ok,
            "median_us": statistics.median(ours) * 1e6 if ours else None,
            "p10_us": sorted(ours)[len(ours) // 10] * 1e6 if ours else None,
            "p90_us": sorted(ours)[9 * len(ours) // 10] * 1e6 if ours else None,

@@ -143,7 +143,7 @@ def cpu_stream_baseline(cfg, x, budget_s):
     while True:
         h = x[:n].cpu().numpy()
         t0 = time.perf_counter()
-        pbs = O.stream_walk(cfg, h)
+        pbs = O.stream_walk_ring(cfg, h)[0]
         for pb in pbs:
             if pb + span <= len(h):
                 O.decode_frame(cfg, h[pb:pb + span])
@@ -152,7 +152,7 @@ def cpu_stream_baseline(cfg, x, budget_s):
             break
         n = min(len(x), n * 2)
     return {"value": n / dt, "unit": "stream samples/s", "cores": 1, "kind": "port",
-            "sample": f"oracle orc_stream_walk + orc_decode_frame (own FFT; FFTW absent) over the first "
+            "sample": f"oracle orc_stream_walk_ring + orc_decode_frame (own FFT; FFTW absent) over the first "
                       f"{n} samples ({len(pbs)} frames) of the same stream, {dt:.1f} s, 1 thread"}
 
 
