@@ -1857,6 +1857,9 @@ int ofdm_set_walk_tuning(ofdm_ctx* c, const ofdm_walk_tuning* t)
     if (!c || !t) return fail(OFDM_ERR_INVALID, "null argument");
     if (t->chunks_per_slot < 1 || t->halo_milli < 0 || t->ext_milli < 0 || !(t->t2_margin >= 0.0))
         return fail(OFDM_ERR_INVALID, "walk tuning out of range");
+    if (t->t2_margin < 4e-5 && !t->allow_uncertified)
+        return fail(OFDM_ERR_INVALID, "t2_margin %g is below the certified 4e-5 (the walk could differ from the "
+                                      "reference); allow_uncertified = 1 is a test-only switch", t->t2_margin);
     c->walk = *t;
     return OFDM_OK;
 }

@@ -57,7 +57,8 @@ class Channel(C.Structure):
 class WalkTuning(C.Structure):
     """ofdm_walk_tuning: per-context stream walker settings (tests, experiments)."""
     _fields_ = [("chunks_per_slot", C.c_long), ("halo_milli", C.c_long), ("ext_milli", C.c_long),
-                ("exact_search", C.c_int), ("t2_f32", C.c_int), ("t2_margin", C.c_double)]
+                ("exact_search", C.c_int), ("t2_f32", C.c_int), ("t2_margin", C.c_double),
+                ("allow_uncertified", C.c_int)]
 
 
 class WalkState(C.Structure):

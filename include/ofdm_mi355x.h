@@ -425,15 +425,18 @@ int ofdm_stream_shard_margins(const ofdm_ctx* ctx, long* halo_out, long* tail_ou
  * preamble search by the reference's serial recurrence; t2_f32 = 0 turns the
  * FP32 T2 screen off (FP64 only). t2_margin is the FP32 screen's
  * certification margin: at or above the default 4e-5 every uncertain block is
- * decided in FP64; a smaller margin trusts raw FP32 ratios near the level and
- * can make the walk differ from the reference (tests use 0 and 1). */
+ * decided in FP64. A smaller margin would trust raw FP32 ratios near the
+ * level and could make the walk differ from the reference, so it is refused
+ * (OFDM_ERR_INVALID) unless allow_uncertified = 1, a test-only switch (the
+ * tests compare margin 0 against the certified screen). */
 typedef struct ofdm_walk_tuning {
     long chunks_per_slot; /* chunks per resident walker (>= 1; default 1)       */
     long halo_milli;      /* walk-in halo, 1/1000 frames (default 3000)         */
     long ext_milli;       /* walk-on past the core end, 1/1000 frames (0)       */
     int exact_search;     /* 1: serial-recurrence preamble search (default 0)   */
     int t2_f32;           /* 1: certified FP32 T2 screen (default 1)            */
-    double t2_margin;     /* FP32 screen margin (default 4e-5)                  */
+    double t2_margin;     /* FP32 screen margin (default 4e-5, the certified minimum) */
+    int allow_uncertified; /* test only: 1 accepts t2_margin < 4e-5 (default 0) */
 } ofdm_walk_tuning;
 int ofdm_walk_tuning_default(ofdm_walk_tuning* out);
 int ofdm_get_walk_tuning(const ofdm_ctx* ctx, ofdm_walk_tuning* out);

@@ -10,6 +10,8 @@ data/*.bin, data.txt), re-encoded compactly. No reference source is copied.
   data/t2_sin_corr.bin      -> t2_sin_corr.npy       (963 f64)
   data/phases.bin           -> phases.npy            (256 complex128)
   data/constell.bin         -> constell.npy          (2048 complex128)
+  data/row.bin              -> row.npy               (5760 complex128, verbatim: a preamble+message region,
+                                                      BASELINE config 4's named input)
   data.txt                  -> data_txt.bin          (248-B decoded payload)
   derived (verified by tests/test_oracle_golden.py): golden.json
 """
@@ -32,6 +34,7 @@ def main():
     np.save(os.path.join(HERE, "phases.npy"), np.fromfile(os.path.join(REF, "data/phases.bin")).view(np.complex128))
     np.save(os.path.join(HERE, "constell.npy"),
             np.fromfile(os.path.join(REF, "data/constell.bin")).view(np.complex128))
+    np.save(os.path.join(HERE, "row.npy"), np.fromfile(os.path.join(REF, "data/row.bin")).view(np.complex128))
     with open(os.path.join(REF, "data.txt"), "rb") as f:
         payload = f.read()
     with open(os.path.join(HERE, "data_txt.bin"), "wb") as f:

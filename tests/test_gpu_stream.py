@@ -171,7 +171,7 @@ def test_stream_walk_certified_search_equals_serial_recurrence():
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("tuning", [dict(t2_margin=1.0), dict(t2_f32=0), dict(t2_margin=0.0)])
+@pytest.mark.parametrize("tuning", [dict(t2_margin=1.0), dict(t2_f32=0), dict(t2_margin=0.0, allow_uncertified=1)])
 def test_stream_walk_fp32_t2_screen_equals_fp64(tuning):
     # the walker's certified FP32 T2 screen against FP64 only: margin 1 makes
     # every block uncertain (each scan step re-evaluated by the FP64 path),
@@ -341,6 +341,9 @@ def test_walk_tuning_defaults_and_validation():
         m.walk_tuning(chunks_per_slot=0)
     with pytest.raises(M.OfdmError):
         m.walk_tuning(t2_margin=-1.0)
+    with pytest.raises(M.OfdmError, match="certified"):
+        m.walk_tuning(t2_margin=1e-5)  # below the certified margin: refused in production
+    m.walk_tuning(t2_margin=1e-5, allow_uncertified=1)  # the test-only switch
     m.walk_tuning()  # back to the defaults
 
 
