@@ -242,9 +242,9 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, tx_min_blocks(LOGN, I16)) tx_
 
     // FFT_FORM::write layout (Frame.cpp:31-44,54-62) as per-bin codes: data
     // index, payload-symbol mask, table base (ofdm_internal.hpp tx_code)
-    int code[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) code[i] = a.tab.tx_code[t + T * i];
+    // the per-bin codes are re-read per symbol (L1/L2-resident 4*N bytes)
+    // rather than held across the symbol loop: 8 fewer VGPRs live across the
+    // transform and the emit
 
     const long nsym = a.nframes * a.S;
     const int k = a.k;
@@ -261,11 +261,15 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, tx_min_blocks(LOGN, I16)) tx_
     // decoded), so neither side needs per-lane guards.
     const bool by_word = (bps & 3) == 0 && (a.bytes_per_frame & 3) == 0 && ((uintptr_t)a.bytes & 3) == 0;
     const int nwords = bps >> 2;
-    const int wi0 = t < nwords ? t : 0, wi1 = t + T < nwords ? t + T : 0;
     uint32_t nb[8];
     auto fetch = [&](long s) {
         const uint8_t* src = sym_bytes(s);
         if (by_word) {
+            // word indices from an opaque copy of the thread index (not held
+            // across the symbol loop)
+            int tt;
+            asm volatile("v_mov_b32 %0, %1" : "=v"(tt) : "v"(t));
+            const int wi0 = tt < nwords ? tt : 0, wi1 = tt + T < nwords ? tt + T : 0;
             const uint32_t* w = reinterpret_cast<const uint32_t*>(src);
             nb[0] = w[wi0];
             nb[1] = w[wi1];
@@ -307,6 +311,15 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, tx_min_blocks(LOGN, I16)) tx_
         // Modulation::mod: k-bit symbol -> constellation point (modulation.cpp:39-50);
         // pilots = pilot_ampl, unused bins 0 (Frame.cpp:56-62)
         double2 v[8];
+        int code[8];
+        {
+            // opaque copy of the thread index: the loads stay in the loop
+            int tt;
+            asm volatile("v_mov_b32 %0, %1" : "=v"(tt) : "v"(t));
+            const int* ct = a.tab.tx_code + tt;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) code[i] = ct[T * i];
+        }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int d = code[i] & 0x1fff, m = (code[i] >> 13) & 0xff, base = code[i] >> 21;
@@ -360,13 +373,17 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, tx_min_blocks(LOGN, I16)) tx_
             for (int i = 0; i < 8; ++i)
                 if (i >= i_cp) emit(t + T * i - (N - a.cp), v[i]);
         } else {
-            // general cp: the tail of the symbol through the LDS image
+            // general cp: the tail of the symbol through the LDS image (its
+            // addresses from an opaque copy of the thread index, so they are
+            // not hoisted out of the symbol loop and held live for this rare path)
+            int tt;
+            asm volatile("v_mov_b32 %0, %1" : "=v"(tt) : "v"(t));
             lds_barrier();  // every thread has read the last pass's inputs
 #pragma unroll
             for (int i = 0; i < 8; ++i)
-                if (t + T * i >= N - a.cp) fft[lds_swz(t + T * i)] = v[i];
+                if (tt + T * i >= N - a.cp) fft[lds_swz(tt + T * i)] = v[i];
             lds_barrier();
-            for (int j = t; j < a.cp; j += T) emit(j, fft[lds_swz(N - a.cp + j)]);
+            for (int j = tt; j < a.cp; j += T) emit(j, fft[lds_swz(N - a.cp + j)]);
         }
 #pragma unroll
         for (int i = 0; i < 8; ++i) emit(a.cp + t + T * i, v[i]);
