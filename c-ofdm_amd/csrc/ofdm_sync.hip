@@ -2293,10 +2293,18 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
     int* bestg = best + 1;
     int* unsure = best + 2;
     double* scr = reinterpret_cast<double*>(best + 4);  // 16 scan / max scratch
-    // T2 first-hit block, two slots used alternately (one barrier per scan
-    // step), in scr[4] (the preamble search's answer is scr[2]): the
-    // walker's LDS stays at 4 walkers per CU
-    int* bslot = reinterpret_cast<int*>(scr + 4);  // [0..1] first hit, [2..3] first uncertain (FP32 screen)
+    // T2 first-hit block, three slots used in turn (one barrier per scan
+    // step), in scr[4..6] (the preamble search's answer is scr[2]): the
+    // walker's LDS stays at 4 walkers per CU. Evaluation k collects into slot
+    // k % 3 and, BEFORE its barrier, thread 0 resets slot (k + 1) % 3 for the
+    // next one: every thread read that slot (evaluation k - 2's answer)
+    // before evaluation k - 1's barrier, and evaluation k + 1's atomics
+    // follow evaluation k's barrier. (With two slots reset after the barrier,
+    // a wave running ahead into the next evaluation could post its hit before
+    // a starved thread 0 reset the slot, and the hit was lost: a frame
+    // skipped. Streams with exact-zero gaps, whose every zero block the FP32
+    // screen sends to FP64, met it.)
+    int* bslot = reinterpret_cast<int*>(scr + 4);  // [0..2] first hit, [3..5] first uncertain (FP32 screen)
     double2* tw_m = reinterpret_cast<double2*>(scr + 16);  // TwLds<WALK_FFT_LOGM> (FFT search)
     double2* big = tw_m + TwLds<WALK_FFT_LOGM>::SIZE;
     double2* fftb = big;                                // G * N (T2 transforms)
@@ -2312,12 +2320,9 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
     if (a.tspec) load_twiddles<WALK_FFT_LOGM>(a.tw_m, tw_m, t0, WT);
     if (t0 == 0) {
         *bestg = INT_MAX;
-        bslot[0] = INT_MAX;
-        bslot[1] = INT_MAX;
-        bslot[2] = INT_MAX;
-        bslot[3] = INT_MAX;
+        for (int i = 0; i < 6; ++i) bslot[i] = INT_MAX;
     }
-    unsigned scan_it = 0;  // T2 scan steps so far (uniform): picks the bslot
+    int sl = 0;  // the slot of the next T2 evaluation (uniform; cycles 0, 1, 2)
     // chunks: from the queue until it is drained (walkers that run slower on
     // their CU take fewer), or the workgroup's one chunk
     for (int round = 0;; ++round) {
@@ -2393,8 +2398,8 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
         bool stop = false;
         // FP64: G blocks from `base` (block g per group of T threads); the
         // first block whose ratio exceeds the level (Frame.hpp:150-197), or
-        // INT_MAX. Slot scan_it & 1 collects the first hit; the other slot was
-        // read before this evaluation's barrier and is reset for the next.
+        // INT_MAX. Slot sl collects the first hit; slot sl + 1 (mod 3) is reset
+        // for the next evaluation before this one's barrier.
         auto t2_eval64 = [&](long base) -> int {
             // opaque per-evaluation copy of the thread's index in its group:
             // the pass addresses and bin masks are derived here, not hoisted
@@ -2444,15 +2449,16 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
                     sine += red[g * NW + w].y;
                 }
             }
-            int* hslot = bslot + (scan_it & 1);
+            int* hslot = bslot + sl;
+            const int nx = sl == 2 ? 0 : sl + 1;
+            if (t == 0) bslot[nx] = INT_MAX;
             if (tt == 0 && live && tot != 0.0) {
                 const double rel = sine / tot;
                 if (!isnan(rel) && rel > a.t2_level) atomicMin(hslot, g);
             }
             __syncthreads();
             const int bg = *hslot;
-            if (t == 0) bslot[(scan_it + 1) & 1] = INT_MAX;
-            ++scan_it;
+            sl = nx;
             return bg;
         };
         // checks before a scan step from `base` (the walk state is (base, rend)):
@@ -2549,8 +2555,13 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
                         if (rel <= lev - marg) return 0;
                         return 2;
                     };
-                    int* hslot = bslot + (scan_it & 1);
-                    int* uslot = bslot + 2 + (scan_it & 1);
+                    int* hslot = bslot + sl;
+                    int* uslot = bslot + 3 + sl;
+                    const int nx = sl == 2 ? 0 : sl + 1;
+                    if (t == 0) {
+                        bslot[nx] = INT_MAX;
+                        bslot[3 + nx] = INT_MAX;
+                    }
                     if (tt == 0) {
                         const int da = screen(liveA, ta, sa), db = screen(liveB, tb, sb);
                         if (da) atomicMin(hslot, g);
@@ -2561,11 +2572,7 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
                     __syncthreads();
                     int bg = *hslot;
                     const int bu = *uslot;
-                    if (t == 0) {
-                        bslot[(scan_it + 1) & 1] = INT_MAX;
-                        bslot[2 + ((scan_it + 1) & 1)] = INT_MAX;
-                    }
-                    ++scan_it;
+                    sl = nx;
                     if (bg != INT_MAX && bu == bg) {  // uniform: this step's decision in FP64
                         bg = t2_eval64(base);
                         if (bg == INT_MAX) {

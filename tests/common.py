@@ -83,6 +83,25 @@ def impaired_stream(cfg, nf, seed, snr_db=20.0, cfo_max=0.004, gap_max=4096):
     return O.awgn(x, 10 ** (-snr_db / 20), seed=seed), data
 
 
+def capture_stream(cfg, nf, seed, gap_max=3000):
+    """A wire capture as tx.cpp + the SDR stand-in make it (data/tx.bin
+    layout): full frames in FRAME_FORM::get_int16 scaling (x mult), exact-zero
+    silences of 0..gap_max samples between them (no noise), one frame_len of
+    zeros at the end. Returns (complex128 samples, interleaved int16)."""
+    g = O.geometry(cfg)
+    rng = np.random.default_rng(seed)
+    data = payload(nf * g["bytes_per_frame"], seed)
+    parts = []
+    for f in range(nf):
+        fr = O.frame_write(cfg, data[f * g["bytes_per_frame"]:(f + 1) * g["bytes_per_frame"]])
+        parts += [np.zeros((int(rng.integers(0, gap_max + 1)), 2), np.int16),
+                  O.get_int16(fr, cfg["mult"]).reshape(-1, 2)]
+    parts.append(np.zeros((g["frame_len"], 2), np.int16))
+    x16 = np.ascontiguousarray(np.concatenate(parts).reshape(-1))
+    w = x16.astype(np.float64)
+    return w[0::2] + 1j * w[1::2], x16
+
+
 def decision_thresholds(k):
     """Modulation::demod's cell edges on each axis (modulation.cpp:53-87)."""
     m = 1 << (k // 2)

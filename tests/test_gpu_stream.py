@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from common import B, D, G, golden, impaired_stream, payload, rel_err
+from common import B, D, G, capture_stream, golden, impaired_stream, payload, rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -125,7 +125,27 @@ def test_stream_ring_walk_matches_rx_cpp_loop(rcfg, chunk):
     x, data = impaired_stream(rcfg, 40, seed=4)
     want = check_against_oracle(rcfg, x, run_stream(rcfg, x, chunk=chunk))
     assert np.array_equal(want, O.rx_app_walk(rcfg, x))  # rx.cpp's loop on a real ring buffer
-    assert not np.array_equal(want, O.stream_walk(rcfg, x))  # the ring loses frames here
+
+
+@pytest.mark.parametrize("ring", [None, 0], ids=["ring", "continuous"])
+@pytest.mark.parametrize("chunk", [0, 20000, 2000000])
+def test_stream_wire_capture_with_exact_zero_gaps(ring, chunk):
+    """A capture as tx.cpp writes it (int16 scaling, exact-zero silences, no
+    noise): every zero T2 block is uncertain for the FP32 screen and goes to
+    the FP64 evaluation, back to back with the screen's steps (the slot
+    protocol of the T2 first hit is exercised on every step). f64 and int16
+    input, whole-walker and chunked."""
+    x, x16 = capture_stream(D, 120, seed=4)
+    want = check_against_oracle(D, x, run_stream(D, x, chunk=chunk, max_frames=256, ring=ring), ring=ring)
+    assert len(want) >= 110
+    m = modem(D)
+    old = m.stream_ring(ring) if ring is not None else None
+    try:
+        got = run_stream_i16(D, x16, max_frames=256, chunk=chunk)
+    finally:
+        if old is not None:
+            m.stream_ring(old)
+    assert got[0] == len(want) and np.array_equal(got[1], want)
 
 
 @pytest.mark.parametrize("halo,ext", [(0, 0), (250, 0), (100, 2000)])
