@@ -1580,7 +1580,9 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
             // 512, 640-point CFO form: sync stage + rx stage per frame, the
             // ramps and channel through LDS); else pilot_freq_sinh + the
             // params stage (one kernel or two), then the stream rx.
-            hipError_t e2 = ofdm::launch_stream_decode(ca, sa, ra, c->logn, pl->logm, pl->g, st);
+            hipError_t e2 = c->walk.staged_decode
+                                ? hipErrorNotSupported
+                                : ofdm::launch_stream_decode(ca, sa, ra, c->logn, pl->logm, pl->g, st);
             if (e2 == hipErrorNotSupported) {
                 // other geometries: pilot_freq_sinh, the params stage, then
                 // the stream rx (two waves per frame at N = 512)
@@ -1855,6 +1857,7 @@ int ofdm_get_walk_tuning(const ofdm_ctx* c, ofdm_walk_tuning* o)
 int ofdm_set_walk_tuning(ofdm_ctx* c, const ofdm_walk_tuning* t)
 {
     if (!c || !t) return fail(OFDM_ERR_INVALID, "null argument");
+    if (t->staged_decode != 0 && t->staged_decode != 1) return fail(OFDM_ERR_INVALID, "staged_decode must be 0 or 1");
     if (t->chunks_per_slot < 1 || t->halo_milli < 0 || t->ext_milli < 0 || !(t->t2_margin >= 0.0))
         return fail(OFDM_ERR_INVALID, "walk tuning out of range");
     if (t->t2_margin < 4e-5 && !t->allow_uncertified)

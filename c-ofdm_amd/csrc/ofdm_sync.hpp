@@ -208,6 +208,12 @@ hipError_t launch_stream_params(int logn, const StreamParamsArgs& a, hipStream_t
 hipError_t launch_stream_decode(const CfoArgs& c, const StreamParamsArgs& a, const RxArgs& r, int logn, int logm, int g,
                                 hipStream_t st);
 
+// the same for N = 2048 / 4096 with cp = N/4 and a 5 x N/4-point CFO form
+// (ofdm_stream_wide.hip): whether the geometry fits, and the launch
+bool stream_decode_wide_fits(const StreamParamsArgs& a, int logn, int logm, int g, int cfo_p);
+hipError_t launch_stream_decode_wide(const CfoArgs& c, const StreamParamsArgs& a, const RxArgs& r, int logn,
+                                     hipStream_t st);
+
 hipError_t launch_stream_walk(int logt, const WalkArgs& a, long nblocks, hipStream_t st);
 // stream walkers resident at once on the current device (occupancy of the
 // walker with this geometry's LDS: 8 per CU for the default geometries)

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define OFDM_MI355X_ABI_VERSION 2
+#define OFDM_MI355X_ABI_VERSION 3
 
 enum {
     OFDM_OK = 0,
@@ -428,7 +428,9 @@ int ofdm_stream_shard_margins(const ofdm_ctx* ctx, long* halo_out, long* tail_ou
  * decided in FP64. A smaller margin would trust raw FP32 ratios near the
  * level and could make the walk differ from the reference, so it is refused
  * (OFDM_ERR_INVALID) unless allow_uncertified = 1, a test-only switch (the
- * tests compare margin 0 against the certified screen). */
+ * tests compare margin 0 against the certified screen). staged_decode = 1
+ * decodes through the three staged kernels instead of the one fused decode
+ * kernel (same results within the parity bar; for A/B measurements). */
 typedef struct ofdm_walk_tuning {
     long chunks_per_slot; /* chunks per resident walker (>= 1; default 1)       */
     long halo_milli;      /* walk-in halo, 1/1000 frames (default 3000)         */
@@ -437,6 +439,9 @@ typedef struct ofdm_walk_tuning {
     int t2_f32;           /* 1: certified FP32 T2 screen (default 1)            */
     double t2_margin;     /* FP32 screen margin (default 4e-5, the certified minimum) */
     int allow_uncertified; /* test only: 1 accepts t2_margin < 4e-5 (default 0) */
+    int staged_decode;    /* 1: decode located frames with the staged cfo ->
+                             params -> rx kernels even where a fused decode
+                             kernel fits (A/B measurements, tests; default 0) */
 } ofdm_walk_tuning;
 int ofdm_walk_tuning_default(ofdm_walk_tuning* out);
 int ofdm_get_walk_tuning(const ofdm_ctx* ctx, ofdm_walk_tuning* out);

@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from common import B, D, G, capture_stream, golden, impaired_stream, payload, rel_err
+from common import CC, B, D, G, capture_stream, golden, impaired_stream, payload, rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -257,6 +257,35 @@ def test_stream_config_b_and_payload_roundtrip():
     assert nf >= 6 and all(any(np.array_equal(o, fr) for fr in frames) for o in out)
 
 
+@pytest.mark.parametrize("name", ["B", "C"])
+def test_stream_wide_fused_decode_matches_oracle_and_staged(name):
+    # configs B / C (N = 2048 / 4096, cp = N/4): the located frames decode
+    # through the fused wide kernel (ofdm_stream_wide.hip); staged_decode = 1
+    # takes the cfo -> params -> rx kernels. Both against the oracle, every
+    # frame (CFO and bytes exact, constellation 1e-9, no decision flips)
+    cfg = {"B": B, "C": CC}[name]
+    x, data = impaired_stream(cfg, 10, seed=21)
+    fused = run_stream(cfg, x, chunk=40000)
+    want = check_against_oracle(cfg, x, fused)
+    staged = run_stream(cfg, x, chunk=40000, tuning=dict(staged_decode=1))
+    check_against_oracle(cfg, x, staged)
+    assert len(want) >= 5
+    assert np.array_equal(fused[2], staged[2]) and np.array_equal(fused[4], staged[4])
+    assert rel_err(fused[3], staged[3]) < 1e-9
+
+
+def test_stream_wide_fused_decode_i16_equals_f64():
+    x, _ = impaired_stream(B, 10, seed=22)
+    x16 = to_i16(x * 200.0)
+    xd = x16[0::2].astype(np.float64) + 1j * x16[1::2].astype(np.float64)
+    got = run_stream_i16(B, x16, chunk=40000)
+    ref = run_stream(B, xd, chunk=40000)
+    assert got[0] == ref[0] and got[0] >= 5
+    for a, b in zip(got[1:], ref[1:4]):
+        assert np.array_equal(a, b)
+    check_against_oracle(B, xd, ref)
+
+
 def test_stream_edges():
     g = O.geometry(D)
     # no frames: noise only, and a stream shorter than one T2 block
@@ -364,6 +393,9 @@ def test_walk_tuning_defaults_and_validation():
     with pytest.raises(M.OfdmError, match="certified"):
         m.walk_tuning(t2_margin=1e-5)  # below the certified margin: refused in production
     m.walk_tuning(t2_margin=1e-5, allow_uncertified=1)  # the test-only switch
+    assert t.staged_decode == 0
+    with pytest.raises(M.OfdmError):
+        m.walk_tuning(staged_decode=2)
     m.walk_tuning()  # back to the defaults
 
 
