@@ -91,7 +91,7 @@ __global__ void __launch_bounds__(WideGeo<LOGN>::NT, 4) stream_decode_wide_kerne
     double2* A = tw + TwLds<LOGN>::SIZE;  // 2N: the two transform images
     double2* pil = A + 2 * N;             // S*P raw pilots (rx stage)
     double2* rtg = pil + S * P;           // the ramp table (sync -> rx), then the gains
-    double2* misc = rtg + (S * P > RTS * S ? S * P : RTS * S);  // {b, aa}
+    double2* misc = rtg + (S * P > RTS * S ? S * P : RTS * S);  // {b, aa}, e^{-i phi_pr}
     double2* dat = A + 5 * M;
     double* ph = reinterpret_cast<double*>(A + 3 * N / 2);
     double2* twm = A + SL::TWM;
@@ -99,7 +99,6 @@ __global__ void __launch_bounds__(WideGeo<LOGN>::NT, 4) stream_decode_wide_kerne
     double2* red = A + SL::RED;
     double2* cps = A + SL::CPS;
     double* phi = reinterpret_cast<double*>(A + SL::PHI);
-    double* psi = reinterpret_cast<double*>(A + SL::PSI);
     int* wsum = reinterpret_cast<int*>(A + SL::WSUM);
 
     const long f = blockIdx.x;
@@ -110,6 +109,11 @@ __global__ void __launch_bounds__(WideGeo<LOGN>::NT, 4) stream_decode_wide_kerne
     const long x0 = a.starts[f];
 
     // ------------------------------------------------------------ pilot_freq_sinh
+    // The CFO transforms occupy the first CFO_W waves; the others meanwhile
+    // sum the CP correlations (cp_freq_sinh's raw sums need no CFO: the
+    // rotation by e^{-2 pi i cfo N} is applied to the sum afterwards).
+    constexpr int CFO_W = G * TM / 64;
+    static_assert(CFO_W < NW, "waves left for the CP sums");
     __builtin_amdgcn_s_setprio(1);  // the sync stage's chains ahead of the other frame's transforms
     {
         // the combine twiddles first (in-order vector-memory returns)
@@ -119,15 +123,47 @@ __global__ void __launch_bounds__(WideGeo<LOGN>::NT, 4) stream_decode_wide_kerne
         const double2 w1 = c.tw_full[M], w2 = c.tw_full[2 * M];
         // transform g holds x[G*n + g], n = tt + TM*i (groups of whole waves)
         const int g = tid / TM, tt = tid % TM;
-        const bool act = g < G;  // wave-uniform
+        const bool act = w < CFO_W;  // wave-uniform
         double2 v[8];
+        if (act) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-            v[i] = act ? src_sample(c.x, c.x16, x0 + (long)G * (tt + TM * i) + g) : make_double2(0.0, 0.0);
+            for (int i = 0; i < 8; ++i) v[i] = src_sample(c.x, c.x16, x0 + (long)G * (tt + TM * i) + g);
+        }
         load_twiddles<LOGN>(a.tab.tw, tw, tid, NT);
-        load_twiddles<LOGM>(c.tw_sub, twm, tid, NT);
-        __syncthreads();  // twiddles visible
-        fft_block_active<LOGM, -1>(v, tt, twm, A + (act ? g : 0) * M, act);
+        if constexpr (TM == 64) {
+            // one wave per transform: each CFO wave writes the whole M-point
+            // table itself (the same values at the same addresses), so its own
+            // LDS wait publishes it, and the transforms sync within their wave
+            if (act) {
+                load_twiddles<LOGM>(c.tw_sub, twm, lane, 64);
+                wave_lds_sync();
+                fft_block_wave<LOGM, -1>(v, tt, twm, A + g * M);
+            }
+        } else {
+            load_twiddles<LOGM>(c.tw_sub, twm, tid, NT);
+            __syncthreads();  // twiddles visible
+        }
+        if (!act) {
+            // symbol q (0: the preamble): sum_j conj(x[qL + j]) x[qL + j + N], j < cp
+            for (int q = w - CFO_W; q < Q; q += NW - CFO_W) {
+                double2 acc = make_double2(0.0, 0.0);
+#pragma unroll 4
+                for (int j = lane; j < CP; j += 64) {
+                    const long i0 = x0 + (long)q * L + j;
+                    acc = cadd(acc, cconj_mul(src_sample(a.iq, a.iq16, i0), src_sample(a.iq, a.iq16, i0 + N)));
+                }
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    acc.x += __shfl_xor(acc.x, o);
+                    acc.y += __shfl_xor(acc.y, o);
+                }
+                if (lane == 0) cps[q] = acc;
+            }
+        }
+        if constexpr (TM == 64)
+            __syncthreads();  // the transforms and the CP sums visible
+        else
+            fft_block_active<LOGM, -1>(v, tt, twm, A + (act ? g : 0) * M, act);
         // X[k + M r] = sum_q W_S^{q k} W_G^{q r} F_q[k], k = tid; stored
         // fftshifted: shifted[i] = spec[(i + S/2) % S] (Frame.hpp:300-305)
         double2 tq[G];
@@ -237,23 +273,6 @@ __global__ void __launch_bounds__(WideGeo<LOGN>::NT, 4) stream_decode_wide_kerne
     }
     const double cfo = red[0].x;
 
-    // ------------------------------------------------------------ cp_freq_sinh sums
-    // symbol q (0: the preamble) on wave q mod NW: conj(x[qL + j]) x[qL + j + N], j < cp
-    for (int q = w; q < Q; q += NW) {
-        double2 acc = make_double2(0.0, 0.0);
-#pragma unroll 4
-        for (int j = lane; j < CP; j += 64) {
-            const long i0 = x0 + (long)q * L + j;
-            acc = cadd(acc, cconj_mul(src_sample(a.iq, a.iq16, i0), src_sample(a.iq, a.iq16, i0 + N)));
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            acc.x += __shfl_xor(acc.x, o);
-            acc.y += __shfl_xor(acc.y, o);
-        }
-        if (lane == 0) cps[q] = acc;
-    }
-    __syncthreads();  // the sums visible
     {
         double rs, rc;
         sincospi(-2.0 * cfo * (double)N, &rs, &rc);
@@ -264,17 +283,10 @@ __global__ void __launch_bounds__(WideGeo<LOGN>::NT, 4) stream_decode_wide_kerne
         }
     }
     __syncthreads();  // phases visible
-    if (tid == 0) {
-        double acc = 0.0;
-        for (int q = 0; q < Q; ++q) {
-            psi[q] = acc;
-            acc += phi[q];
-        }
-    }
 
     // ------------------------------------------------------------ preamble (group 0)
     const bool g0 = tid < T;  // wave-uniform
-    double phr, b, aa;
+    double b, aa;
     {
         const int t = tid;
         double2 z[LT], pz = make_double2(0.0, 0.0), dz[4], mpre[4], prc[CT];
@@ -306,6 +318,26 @@ __global__ void __launch_bounds__(WideGeo<LOGN>::NT, 4) stream_decode_wide_kerne
         } else {
 #pragma unroll
             for (int rr = 0; rr < LT; ++rr) z[rr] = make_double2(0.0, 0.0);
+            // group 1, while group 0 runs the preamble chain: the message
+            // symbols' ramp table. Per symbol s, {e^{i(A+Bk)}, k < 8;
+            // e^{i B 8 2^m}, m < NB; e^{i B T}}, one sincos per entry; theta(m)
+            // = A_s + B_s m over the CP-stripped body, freq_shift + cp_freq_sinh
+            // (psi_q = phi_0 + ... + phi_{q-1}, summed in the reference's
+            // order). pr_phase_sinh's common e^{-i phi_pr} is left out here and
+            // applied with the channel divisor (the FFT is linear, and the
+            // gains F[0,p] conj(F[s,p]) / |F[s,p]|^2 do not see a common phase)
+            for (int e = t - T; e < RTS * S; e += T) {
+                const int s = e / RTS, kk = e % RTS, q = 1 + s;
+                double psq = 0.0;
+                for (int r = 0; r < q; ++r) psq += phi[r];
+                const double Aq = -2.0 * M_PI * cfo * (double)((long)q * L + CP) - (psq * L + phi[q] * CP) / N;
+                const double Bq = -2.0 * M_PI * cfo - phi[q] / N;
+                const double th = kk < 8 ? add_rn(Aq, mul_rn(Bq, (double)kk))
+                                         : mul_rn(Bq, kk < 8 + NB ? (double)(8 << (kk - 8)) : (double)T);
+                double sn, cs;
+                sincos(th, &sn, &cs);
+                rtg[e] = make_double2(cs, sn);
+            }
         }
         // body sample t + T i of the preamble is register CT + i
         double2 vv[8];
@@ -325,7 +357,7 @@ __global__ void __launch_bounds__(WideGeo<LOGN>::NT, 4) stream_decode_wide_kerne
             acc = cadd(acc, make_double2(bacc.x * isn, bacc.y * isn));
         }
         acc = block_sum2<NT>(acc, red);  // group 1 adds zeros
-        phr = atan2(acc.y, acc.x);
+        const double phr = atan2(acc.y, acc.x);
         // e^{-i phr} = conj(acc) / |acc| (uniform; sincos for a zero or non-finite sum)
         double2 rot;
         const double ha = hypot(acc.x, acc.y);
@@ -337,6 +369,7 @@ __global__ void __launch_bounds__(WideGeo<LOGN>::NT, 4) stream_decode_wide_kerne
             sincos(-phr, &rs2, &rc2);
             rot = make_double2(rc2, rs2);
         }
+        if (t == 0) misc[1] = rot;
         if (g0) {
             if (t < P) spil[t] = cmul_exact(pz, rot);
 #pragma unroll
@@ -382,18 +415,6 @@ __global__ void __launch_bounds__(WideGeo<LOGN>::NT, 4) stream_decode_wide_kerne
         const double sx = hn * (hn - 1) / 2, sx2 = (hn - 1) * hn * (2 * hn - 1) / 6;
         b = (sums.x - sx * sums.y) / (sx2 - sx * sx);
         aa = sums.y - b * sx;
-    }
-    // the message symbols' ramp table: per symbol s, {e^{i(A+Bk)}, k < 8;
-    // e^{i B 8 2^m}, m < NB; e^{i B T}}: one sincos per entry
-    if (tid < RTS * S) {
-        const int s = tid / RTS, kk = tid % RTS, q = 1 + s;
-        const double Aq = -2.0 * M_PI * cfo * (double)((long)q * L + CP) - (psi[q] * L + phi[q] * CP) / N - phr;
-        const double Bq = -2.0 * M_PI * cfo - phi[q] / N;
-        const double th = kk < 8 ? add_rn(Aq, mul_rn(Bq, (double)kk))
-                                 : mul_rn(Bq, kk < 8 + NB ? (double)(8 << (kk - 8)) : (double)T);
-        double sn, cs;
-        sincos(th, &sn, &cs);
-        rtg[tid] = make_double2(cs, sn);
     }
     if (tid == 0) misc[0] = make_double2(b, aa);
     __syncthreads();  // the table visible; the sync arrays are free
@@ -464,7 +485,7 @@ __global__ void __launch_bounds__(WideGeo<LOGN>::NT, 4) stream_decode_wide_kerne
     }
     // the channel line (chan_char_lq, Frame.hpp:415-434) at carriers tid and
     // tid + NT, as the conjugates of its unit phasors (the divisor's reciprocal)
-    const double2 ba = misc[0];
+    const double2 ba = misc[0], rot = misc[1];
     double2 chv[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -476,7 +497,7 @@ __global__ void __launch_bounds__(WideGeo<LOGN>::NT, 4) stream_decode_wide_kerne
             th = add_rn(add_rn(mul_rn(-ba.x, (double)D) / 2, mul_rn((double)(d - half), ba.x)), ba.y);
         double sn, cs;
         sincos(th, &sn, &cs);
-        chv[u] = make_double2(cs, -sn);
+        chv[u] = cmul_exact(make_double2(cs, -sn), rot);  // and pr_phase_sinh's e^{-i phi_pr}
     }
     // phys_pilot_ampl = sum |pilot| / (P*S*pilot_ampl)   (Frame.cpp:76-80)
     double pacc = 0.0;
@@ -553,7 +574,7 @@ static size_t wide_shm(const StreamParamsArgs& a)
 {
     using W = WideGeo<LOGN>;
     const size_t sp = (size_t)a.S * a.P, rt = (size_t)W::RTS * a.S;
-    return sizeof(double2) * (TwLds<LOGN>::SIZE + 2 * (size_t)W::N + sp + std::max(sp, rt) + 1);
+    return sizeof(double2) * (TwLds<LOGN>::SIZE + 2 * (size_t)W::N + sp + std::max(sp, rt) + 2);
 }
 
 template <int LOGN, bool I16>

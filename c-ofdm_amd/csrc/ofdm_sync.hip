@@ -2172,7 +2172,11 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
     // a wave running ahead into the next evaluation could post its hit before
     // a starved thread 0 reset the slot, and the hit was lost: a frame
     // skipped. Streams with exact-zero gaps, whose every zero block the FP32
-    // screen sends to FP64, met it.)
+    // screen sends to FP64, met it.) Every evaluation, FP64 or FP32, resets
+    // both the hit and the uncertain slot of the next one: the FP64
+    // re-evaluations advance the rotation too, and an uncertain slot left
+    // stale by them let a later FP32 step take an uncertain (zero) block for a
+    // certain T2 hit, whose failed preamble search then skipped a frame.
     int* bslot = reinterpret_cast<int*>(scr + 4);  // [0..2] first hit, [3..5] first uncertain (FP32 screen)
     double2* tw_m = reinterpret_cast<double2*>(scr + 16);  // TwLds<WALK_FFT_LOGM> (FFT search)
     double2* big = tw_m + TwLds<WALK_FFT_LOGM>::SIZE;
@@ -2320,7 +2324,10 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
             }
             int* hslot = bslot + sl;
             const int nx = sl == 2 ? 0 : sl + 1;
-            if (t == 0) bslot[nx] = INT_MAX;
+            if (t == 0) {  // both slots of the next evaluation, whichever kind it is
+                bslot[nx] = INT_MAX;
+                bslot[3 + nx] = INT_MAX;
+            }
             if (tt == 0 && live && tot != 0.0) {
                 const double rel = sine / tot;
                 if (!isnan(rel) && rel > a.t2_level) atomicMin(hslot, g);
