@@ -37,6 +37,7 @@ CONFIG_B = dict(fft_size=2048, num_data_subc=1024, num_pilot_subc=32, cp_size=51
 # config/config.txt (the D config of SURVEY §8): the config-4 stream's frames
 CONFIG_D = dict(CONFIG_B, fft_size=512, num_data_subc=256, num_pilot_subc=8, cp_size=128, mod_type=4)
 STREAM_WORKLOAD = "config4_stream_D_frames_gaps0-4096_cfo0.004_awgn20dB"
+STREAM_WORKLOAD_B = "config4_stream_B_frames_gaps0-4096_cfo0.004_awgn20dB"
 
 
 def rx_bytes_per_symbol(p) -> int:
@@ -182,7 +183,8 @@ def cpu_stream_baseline(p, x_host: np.ndarray, budget_s: float, i16: bool = Fals
                       f"(rx.cpp's loop is single-threaded) on {_cpu_model()}"}
 
 
-def stream_leg(args, dist, dev, world, rank, M, i16: bool):
+def stream_leg(args, dist, dev, world, rank, M, i16: bool, p=None, frames_per_gpu=0, workload=STREAM_WORKLOAD,
+               pipeline=True, staged_ab=False):
     """SURVEY §8d config 4 (BASELINE configs[3]): the streaming receiver (T2
     detection walk + preamble sync + CFO/CP/phase/channel sync + demod,
     ofdm_rx_stream_shard) over a synthetic continuous stream of D-config
@@ -196,9 +198,12 @@ def stream_leg(args, dist, dev, world, rank, M, i16: bool):
     import ofdm_dist
     import ofdm_stream as SS
     import ofdm_synth as Y
-    p = dict(CONFIG_D)
+    # p: another frame geometry (config B's: the wide fused decode); staged_ab:
+    # the same calls again through the staged decode kernels (walk tuning
+    # staged_decode = 1), reported beside the fused figure
+    p = dict(CONFIG_D if p is None else p)
     modem = M.Modem(p, dev.index)
-    layout = Y.StreamLayout(p, args.stream_frames * world)
+    layout = Y.StreamLayout(p, (frames_per_gpu or args.stream_frames) * world)
     # rx.cpp's SDR ring (the config's rx_buf_size, the library's default) and initial state
     rx = SS.ShardedStreamRx(p, layout.n, world, rank, ring=modem.stream_ring(), initial=modem.initial_state())
     nsl = rx.slice_hi - rx.slice_lo
@@ -254,10 +259,30 @@ def stream_leg(args, dist, dev, world, rank, M, i16: bool):
     tot = torch.tensor([n_owned, ok, rx.rewalks], dtype=torch.int64, device=cdev)
     ofdm_dist.reduce_counters(tot, dist)
     tot = tot.cpu().numpy()
+    staged = None
+    if staged_ab:
+        modem.walk_tuning(staged_decode=1)
+        for _ in range(2):
+            rx.run(walk, exchange)
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(args.stream_reps):
+            rx.run(walk, exchange)
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        el_st = ofdm_dist.max_over_ranks(time.perf_counter() - t1, dev, dist)
+        modem.walk_tuning()
+        staged = {"value": layout.n * args.stream_reps / el_st, "unit": "stream samples/s",
+                  "ms_per_call": el_st / args.stream_reps * 1e3, "fused_speedup_per_sample": el_st / elapsed,
+                  "note": "same stream and calls, the located frames decoded by the staged cfo -> params -> rx "
+                          "kernels (walk tuning staged_decode = 1) instead of the fused decode kernel"}
     esz = 4 if i16 else 16
     core = rx.own_hi - rx.own_lo
     alg_rank = core * esz + n_owned * (16 * npts + layout.bpf)  # stream once + outputs
-    workload = STREAM_WORKLOAD + ("_int16" if i16 else "")
+    workload = workload + ("_int16" if i16 else "")
     pmc = load_pmc_stream(workload) if world == 1 else None
     res = {"metric": "stream samples/s (T2 walk + preamble sync + CFO/CP/phase/chan sync + demod), "
                      "config-4 stream", "workload": workload, "value": layout.n * args.stream_reps / elapsed,
@@ -275,7 +300,10 @@ def stream_leg(args, dist, dev, world, rank, M, i16: bool):
                         "algorithmic_bytes_per_call": alg_rank, "avg_call_ms": call_ms,
                         "traffic": (pmc or {}).get("hbm_bytes_per_call")},
            "cpu_baseline": None}
-    if world == 1 and args.stream_pipeline > 1:
+    res["compute"] = decode_compute(p, n_owned, call_ms)
+    if staged is not None:
+        res["staged"] = staged
+    if pipeline and world == 1 and args.stream_pipeline > 1:
         res["pipelined"] = stream_pipelined(args, p, M, dev, modem, layout, rx, walk, outs, x, nsl, cap, i16,
                                             n_owned, exchange, SS)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -286,6 +314,42 @@ def stream_leg(args, dist, dev, world, rank, M, i16: bool):
             res["cpu_baseline"] = {"error": repr(e)}
     modem.close()
     return res
+
+
+FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X_MICROARCH.md: FP64 vector
+
+
+def decode_flops_per_frame(p) -> int:
+    """Useful FP64 flops of one located frame's decode (main.cpp:60-80 on the
+    frame): the radix-5 x 2^m pilot_freq_sinh transform, the preamble body
+    and the message FFTs at 5 N log2 N each, the per-sample phase ramps (one
+    complex product each), the CP correlations, and per data point the
+    equalisation and channel products and the decision. Transcendentals and
+    reductions are left out (a lower bound of the work)."""
+    import math
+    N, cp, D, S = p["fft_size"], p["cp_size"], p["num_data_subc"], p["num_symb"]
+    L = N + cp
+    m = L // 5
+    cfo = 5 * (5 * m * math.log2(m)) + m * 44 if L % 5 == 0 and m & (m - 1) == 0 else 5 * L * math.log2(L)
+    ffts = (S + 1) * 5 * N * math.log2(N)
+    ramps = 6 * N * S + 6 * L
+    cps = 8 * cp * (S + 1)
+    emit = D * S * (6 + 6 + 6)
+    return int(cfo + ffts + ramps + cps + emit)
+
+
+def decode_compute(p, frames: int, call_ms: float) -> dict:
+    """The decode's compute side (VALU-bound: it takes the same time with
+    int16 input at a quarter of the bytes): useful FP64 flop/s over the whole
+    call time (walker included, so a lower bound) against the FP64 vector
+    peak, and the SIMDs' VALU-busy fraction from the committed SQ counters."""
+    f = decode_flops_per_frame(p)
+    ach = f * frames / (call_ms * 1e-3) / 1e12
+    return {"bound": "valu", "flops_per_frame": f, "achieved": ach, "peak": FP64_VALU_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": ach / FP64_VALU_PEAK_TFLOPS,
+            "valu_busy": 0.78 if p["fft_size"] == 512 else None,
+            "note": "flops over the whole call time (walker + decode); valu_busy of the N = 512 fused decode "
+                    "from profiles/r03l_sq_stream.txt (SQ_ACTIVE_INST_VALU / SQ_BUSY_CYCLES per SIMD)"}
 
 
 def stream_pipelined(args, p, M, dev, modem, layout, rx, walk, outs, x, nsl, cap, i16, n_owned, exchange, SS):
@@ -432,6 +496,8 @@ def main():
     ap.add_argument("--stream-reps", type=int, default=10)
     ap.add_argument("--stream-warmup", type=int, default=10, help="untimed stream calls (clocks ramp)")
     ap.add_argument("--stream-cpu-budget", type=float, default=8.0)
+    ap.add_argument("--stream-b-frames", type=int, default=4096,
+                    help="config-B stream frames per GPU for the stream_B sub-record (0: skip)")
     ap.add_argument("--stream-pipeline", type=int, default=2,
                     help="contexts for the stream record's pipelined figure (1: off; one GPU only)")
     ap.add_argument("--no-config3", action="store_true", help="skip the config-3 (config C) sub-record")
@@ -605,6 +671,11 @@ def main():
         torch.cuda.empty_cache()
         result["stream"] = stream_leg(args, dist, dev, world, rank, M, i16=False)
         result["stream_int16"] = stream_leg(args, dist, dev, world, rank, M, i16=True)
+        if args.stream_b_frames > 0:  # the wide-geometry fused decode (config B frames) against the staged kernels
+            torch.cuda.empty_cache()
+            result["stream_B"] = stream_leg(args, dist, dev, world, rank, M, i16=False, p=CONFIG_B,
+                                            frames_per_gpu=args.stream_b_frames, workload=STREAM_WORKLOAD_B,
+                                            pipeline=False, staged_ab=True)
     if not args.no_config3:
         torch.cuda.empty_cache()
         result["config3"] = config3_leg(args, dist, dev, world, rank, M)

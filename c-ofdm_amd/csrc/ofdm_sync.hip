@@ -1420,13 +1420,18 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
         const double slope0 = -2.0 * M_PI * cfo - phi[0] / N;
         double phr;
         {
-            double sn, cs;
+            // the step e^{i slope0 T} by its own sincos. (Round 3 took it as
+            // lane T/2's phasor squared, a shuffle instead of a second sincos
+            // pass: no change in a serial call, but two contexts receiving on
+            // two streams then no longer overlapped one call's walk with the
+            // other's decode: int16 stream 183 -> 162 G samples/s in a
+            // same-box A/B that reverted each part of that change alone,
+            // profiles/r04h_pipelined_rev.json.)
+            double sn, cs, ws, wc;
             sincos(slope0 * (double)t, &sn, &cs);
+            sincos(slope0 * (double)T, &ws, &wc);
             double2 cc = make_double2(cs, sn);
-            // the step e^{i slope0 T} as lane T/2's phasor squared (T = 64):
-            // a shuffle and a product instead of a second sincos pass
-            const double2 ch = make_double2(__shfl(cc.x, T / 2), __shfl(cc.y, T / 2));
-            const double2 wv = cmul_exact(ch, ch);
+            const double2 wv = make_double2(wc, ws);
             double2 acc = make_double2(0.0, 0.0);
 #pragma unroll
             for (int r = 0; r < RMAX; ++r) {

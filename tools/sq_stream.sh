@@ -13,7 +13,7 @@ acc = collections.defaultdict(list)
 for f in sorted(glob.glob('gpurun_out/ss*/run_counter_collection.csv')):
     for r in csv.DictReader(open(f)):
         k = r['Kernel_Name']
-        for key in ('stream_walk_kernel', 'stream_params_kernel', 'rx_kernel', 'cfo_kernel', 'stream_decode_kernel', 'stream_sync_kernel', 'rx_stream2_kernel', 'compact_kernel'):
+        for key in ('stream_walk_kernel', 'stream_decode_wide_kernel', 'stream_params_kernel', 'rx_kernel', 'cfo_kernel', 'stream_decode_kernel', 'stream_sync_kernel', 'rx_stream2_kernel', 'compact_kernel'):
             if key in k:
                 tmpl = k[k.find(key):k.find('>') + 1]
                 acc[(tmpl, r['Counter_Name'])].append(float(r['Counter_Value']))
