@@ -65,10 +65,16 @@ def test_bench_stream_record_with_pipelined_figure():
     # per-call record, and the two-context pipelined figure whose outputs equal
     # the serial calls'
     r = _bench("--steps", "1", "--warmup", "1", "--frames", "64", "--no-cpu-baseline", "--no-config3",
-               "--stream-frames", "512", "--stream-reps", "2", "--stream-warmup", "1")
+               "--stream-frames", "512", "--stream-reps", "2", "--stream-warmup", "1", "--stream-b-frames", "96")
     for key in ("stream", "stream_int16"):
         s = r[key]
         assert s["value"] > 0 and s["frames_found"] >= 0.95 * s["frames_sent"]
         pp = s["pipelined"]
         assert pp["contexts"] == 2 and pp["calls"] == 4 and pp["outputs_match_serial"] is True
         assert pp["value"] > 0
+        assert s["compute"]["bound"] == "valu" and 0 < s["compute"]["frac"] < 1
+    # config-B frames: the wide fused decode, with the staged kernels' figure beside it
+    b = r["stream_B"]
+    assert b["workload"].startswith("config4_stream_B") and b["frames_found"] >= 0.95 * b["frames_sent"]
+    assert b["frames_error_free"] >= 0.95 * b["frames_found"] and "pipelined" not in b
+    assert b["staged"]["value"] > 0 and b["staged"]["fused_speedup_per_sample"] > 0
