@@ -13,8 +13,9 @@ mkdir -p $B $R/abtest
 H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -munsafe-fp-atomics -I$SRC/include $FLAGS"
 $H -c $SRC/c-ofdm_amd/csrc/ofdm_kernels.hip -o $B/k.o &
 $H -c $SRC/c-ofdm_amd/csrc/ofdm_sync.hip -o $B/s.o &
+[ -f $SRC/c-ofdm_amd/csrc/ofdm_stream_wide.hip ] && $H -c $SRC/c-ofdm_amd/csrc/ofdm_stream_wide.hip -o $B/w.o &
 $H -x hip -c $SRC/c-ofdm_amd/csrc/ofdm_capi.cpp -o $B/c.o &
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $R/abtest/libofdm_$NAME.so $B/k.o $B/s.o $B/c.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $R/abtest/libofdm_$NAME.so $B/*.o
 rm -rf $B
 echo built abtest/libofdm_$NAME.so
