@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <climits>
 #include <cstdio>
 #include <optional>
 #include <cstdlib>
@@ -246,15 +247,27 @@ int T2SIN_FORM::find_t2sin(complex_vector& signal, int start_index)
     const long n = (long)signal.size();
     if (size <= 0 || start_index < 0 || start_index > n) return -1;
     const long nblocks = (n - start_index) / size;
-    int* df = (int*)ctx_->buf(2, sizeof(int));
     long b0 = 0, w = std::max<long>(16, 2L * ctx_->geo.frame_len / size + 2);
     while (b0 < nblocks) {
         const long nb = std::min(w, nblocks - b0);
         const size_t len = (size_t)nb * size;
         const DevRange x = stage_in(*ctx_, 0, signal.data() + start_index + b0 * size, len * CD);
-        check(ofdm_t2_scan(ctx_->ctx, (const double*)x.d, len, 0, nullptr, df, ctx_->stream()), "ofdm_t2_scan");
-        int first = -1;
-        ctx_->d2h(&first, df, sizeof(int));
+        // the launch's last workgroup writes the answer straight to a pinned
+        // word (no copy launch, no stream synchronisation): poll it. The
+        // detector's tail may still retire when this returns; the next call
+        // on the thread's stream is ordered after it.
+        volatile int* hf = static_cast<volatile int*>(ctx_->engine().stage(sizeof(int)));
+        *hf = INT_MIN;
+        check(ofdm_t2_scan(ctx_->ctx, (const double*)x.d, len, 0, nullptr, const_cast<int*>(hf), ctx_->stream()),
+              "ofdm_t2_scan");
+        const auto t0 = std::chrono::steady_clock::now();
+        int first = INT_MIN;
+        for (long spin = 0; (first = *hf) == INT_MIN; ++spin)
+            if ((spin & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+                ctx_->sync();  // not landed in 200 ms: wait for the stream (errors surface here)
+                first = *hf;
+                break;
+            }
         if (first >= 0) return (int)(start_index + b0 * size + first);
         b0 += nb;
         w *= 2;

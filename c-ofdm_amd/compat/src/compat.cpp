@@ -483,7 +483,9 @@ std::vector<uint8_t> Modulation::demod(complex_vector& in)
         if (ch->demod_armed && (int)mod_index == ch->bits_k && n * sizeof(complex_double) == ch->cons_bytes &&
             nb == ch->bits_bytes) {
             ch->demod_armed = false;
-            check(ofdm_event_synchronize(ctx_->engine().ctx, ch->ev[6]), "ofdm_event_synchronize");
+            // (no event wait: the served OFDM_FORM::fft that armed this
+            // demod already waited for ev[6], after which the rx kernel's
+            // pinned points and decisions are complete)
             if (std::memcmp(in.data(), ch->hcons_eq, ch->cons_bytes) == 0) {
                 std::memcpy(out.data(), ch->hbits, nb);
                 if (modulation != bpsk)  // clamped in place (modulation.cpp:70-75)

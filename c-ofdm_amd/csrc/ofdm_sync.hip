@@ -119,7 +119,10 @@ __global__ void __launch_bounds__(T2Geo<LOGN>::NT) t2_scan_kernel(T2Args a)
         __threadfence();
         if (atomicAdd(a.first_scratch + 1, 1) == (int)gridDim.x - 1) {
             const int m = atomicExch(a.first_scratch, INT_MAX);
-            if (a.first_out) *a.first_out = m == INT_MAX ? -1 : (int)(a.start + (long)m * N);
+            if (a.first_out) {
+                *a.first_out = m == INT_MAX ? -1 : (int)(a.start + (long)m * N);
+                __threadfence_system();  // a pinned host answer is polled by the caller
+            }
             atomicExch(a.first_scratch + 1, 0);
         }
     }

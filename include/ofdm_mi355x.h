@@ -248,8 +248,11 @@ int ofdm_double_to_int16(ofdm_ctx* ctx, const double* in, size_t n, int16_t* out
 /* ---- rx sync front end ----------------------------- */
 /* T2SIN_FORM::corr (Frame.hpp:96-147) over all floor((n-start)/t2sin_size)
  * blocks from `start`: rel_out[b] = energy ratio if > level else 0 (device,
- * nullable). first_out (device int, nullable): T2SIN_FORM::find_t2sin
- * (Frame.hpp:150-197) = start + b*size of the first block above level, or -1. */
+ * nullable). first_out (device int, or page-locked host int from
+ * ofdm_host_alloc; nullable): T2SIN_FORM::find_t2sin (Frame.hpp:150-197) =
+ * start + b*size of the first block above level, or -1, written once by the
+ * launch's last workgroup (system-scope fence after it: a host thread may
+ * poll a pinned first_out instead of synchronising the stream). */
 int ofdm_t2_scan(ofdm_ctx* ctx, const double* iq, size_t n, long start,
                  double* rel_out, int* first_out, void* stream);
 

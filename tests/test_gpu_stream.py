@@ -274,6 +274,29 @@ def test_stream_wide_fused_decode_matches_oracle_and_staged(name):
     assert rel_err(fused[3], staged[3]) < 1e-9
 
 
+WIDE_VARIANTS = {
+    "B_s3": dict(B, num_symb=3),                                   # odd S: group 1 idle in the last step
+    "B_s5_qam16": dict(B, num_symb=5, mod_type=4),
+    "B_d512_p16": dict(B, num_data_subc=512, num_pilot_subc=16),  # D < 4T, half = T
+    "B_p64_s1": dict(B, num_pilot_subc=64, num_symb=1),           # one symbol, P = T/4
+}
+
+
+@pytest.mark.parametrize("name", list(WIDE_VARIANTS))
+def test_stream_wide_fused_decode_geometry_variants(name):
+    # the wide kernel's geometry bounds (S <= 8 with idle group steps, D <= 4T,
+    # P <= T) on impaired streams, every frame against the oracle and the
+    # staged kernels
+    cfg = WIDE_VARIANTS[name]
+    x, data = impaired_stream(cfg, 8, seed=23)
+    fused = run_stream(cfg, x, chunk=40000)
+    want = check_against_oracle(cfg, x, fused)
+    staged = run_stream(cfg, x, chunk=40000, tuning=dict(staged_decode=1))
+    assert len(want) >= 4
+    assert np.array_equal(fused[1], staged[1]) and np.array_equal(fused[2], staged[2])
+    assert np.array_equal(fused[4], staged[4]) and rel_err(fused[3], staged[3]) < 1e-9
+
+
 def test_stream_wide_fused_decode_i16_equals_f64():
     x, _ = impaired_stream(B, 10, seed=22)
     x16 = to_i16(x * 200.0)
