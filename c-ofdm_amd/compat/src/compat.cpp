@@ -4,6 +4,7 @@
 #include <execinfo.h>
 #include <signal.h>
 #include <unistd.h>
+#include <emmintrin.h>
 
 #include <algorithm>
 #include <cmath>
@@ -471,6 +472,24 @@ complex_vector Modulation::mod(std::vector<uint8_t>& in)
     return out;
 }
 
+// One pass over the caller's points: bitwise equality with the served
+// chain's divided points, and (QAM) the in-place clamp to [-1, 1]
+// (modulation.cpp:70-75) as max(-1, v) then min(1, v): MAXPD/MINPD return
+// their second operand for a NaN, so NaN stays NaN as with std::clamp, and
+// -0.0 stays -0.0. Branch-free: noisy points straddle the clamp at random.
+static bool equal_then_clamp(double* p, const double* q, size_t nd, bool clamp)
+{
+    __m128i diff = _mm_setzero_si128();
+    const __m128d lo = _mm_set1_pd(-1.0), hi = _mm_set1_pd(1.0);
+    for (size_t i = 0; i < nd; i += 2) {  // nd even: complex points
+        const __m128d v = _mm_loadu_pd(p + i);
+        diff = _mm_or_si128(diff, _mm_xor_si128(_mm_castpd_si128(v),
+                                                _mm_loadu_si128(reinterpret_cast<const __m128i*>(q + i))));
+        if (clamp) _mm_storeu_pd(p + i, _mm_min_pd(hi, _mm_max_pd(lo, v)));
+    }
+    return _mm_movemask_epi8(_mm_cmpeq_epi8(diff, _mm_setzero_si128())) == 0xffff;
+}
+
 std::vector<uint8_t> Modulation::demod(complex_vector& in)
 {
     const size_t n = in.size(), nb = (n * mod_index + 7) / 8;
@@ -486,14 +505,13 @@ std::vector<uint8_t> Modulation::demod(complex_vector& in)
             // (no event wait: the served OFDM_FORM::fft that armed this
             // demod already waited for ev[6], after which the rx kernel's
             // pinned points and decisions are complete)
-            if (std::memcmp(in.data(), ch->hcons_eq, ch->cons_bytes) == 0) {
+            if (equal_then_clamp(reinterpret_cast<double*>(in.data()),
+                                 reinterpret_cast<const double*>(ch->hcons_eq), 2 * n, modulation != bpsk)) {
                 std::memcpy(out.data(), ch->hbits, nb);
-                if (modulation != bpsk)  // clamped in place (modulation.cpp:70-75)
-                    for (auto& z : in)
-                        z = complex_double(std::clamp(z.real(), -1.0, 1.0),  // NaN stays NaN, as std::clamp
-                                           std::clamp(z.imag(), -1.0, 1.0));
                 return out;
             }
+            // (a mismatch leaves `in` clamped: the demap below decides and
+            // clamps clamped points to the same bytes and values)
         }
     }
     void* dp = ctx_->buf(0, n * sizeof(complex_double));
