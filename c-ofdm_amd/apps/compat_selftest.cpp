@@ -12,6 +12,9 @@
 //   2. form_int16_to_double, find_t2sin, find_preamble and corr on the
 //      mirrored rx ring equal the staged path, also after direct host writes
 //      to from_sdr_buf;
+//      the chain also serves Modulation::demod after rx.cpp's division:
+//      its bytes and in-place clamp equal the unserved demod's, and a point
+//      moved after the division makes it refuse;
 //   3. PREAMBLE_FORM::chan_char equals the reference's formula
 //      (Frame.hpp:375-385) evaluated here on fft()'s output.
 // Usage: compat_selftest <config.txt> [frames]. Prints "SELFTEST OK ...".
@@ -83,6 +86,22 @@ int main(int argc, char** argv)
         CHECK(h1.size() == h2.size() && same(h1.data(), h2.data(), h1.size()), "%s frame %d: chan_char_lq", what, k);
         auto f1 = rx.message.fft(), f2 = msg2.fft();
         CHECK(f1.size() == f2.size() && same(f1.data(), f2.data(), f1.size()), "%s frame %d: fft", what, k);
+        // rx.cpp:214-221: the division by chan_char, then Modulation::demod
+        // (served from the chain's decisions for the mirrored form when the
+        // points are the chain's, bit for bit; every fourth frame one point
+        // is moved after the division, so the served demod must refuse)
+        complex_vector d1(f1), d2(f2);
+        for (size_t j = 0; j < d1.size(); j++) {
+            d1[j] /= h1[j % h1.size()];
+            d2[j] /= h2[j % h2.size()];
+        }
+        if (k % 4 == 2 && d1.size() > 7) {
+            d1[7] += complex_double(1e-3, 0.0);
+            d2[7] += complex_double(1e-3, 0.0);
+        }
+        const bit_vector b1 = rx.message.Mod.demod(d1), b2 = msg2.Mod.demod(d2);
+        CHECK(b1 == b2, "%s frame %d: demod bytes", what, k);
+        CHECK(same(d1.data(), d2.data(), d1.size()), "%s frame %d: demod's in-place clamp", what, k);
     };
 
     std::vector<complex_vector> sent;

@@ -127,7 +127,7 @@ __global__ void __launch_bounds__(WideGeo<LOGN>::NT, 4) stream_decode_wide_kerne
         double2 v[8];
         if (act) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) v[i] = src_sample(c.x, c.x16, x0 + (long)G * (tt + TM * i) + g);
+            for (int i = 0; i < 8; ++i) v[i] = src_sample_t<I16>(c.x, c.x16, x0 + (long)G * (tt + TM * i) + g);
         }
         load_twiddles<LOGN>(a.tab.tw, tw, tid, NT);
         if constexpr (TM == 64) {
@@ -150,7 +150,7 @@ __global__ void __launch_bounds__(WideGeo<LOGN>::NT, 4) stream_decode_wide_kerne
 #pragma unroll 4
                 for (int j = lane; j < CP; j += 64) {
                     const long i0 = x0 + (long)q * L + j;
-                    acc = cadd(acc, cconj_mul(src_sample(a.iq, a.iq16, i0), src_sample(a.iq, a.iq16, i0 + N)));
+                    acc = cadd(acc, cconj_mul(src_sample_t<I16>(a.iq, a.iq16, i0), src_sample_t<I16>(a.iq, a.iq16, i0 + N)));
                 }
 #pragma unroll
                 for (int o = 32; o > 0; o >>= 1) {
@@ -302,7 +302,7 @@ __global__ void __launch_bounds__(WideGeo<LOGN>::NT, 4) stream_decode_wide_kerne
 #pragma unroll
             for (int u = 0; u < CT; ++u) prc[u] = a.pre[t + T * u];
 #pragma unroll
-            for (int rr = 0; rr < LT; ++rr) z[rr] = src_sample(a.iq, a.iq16, x0 + t + (long)T * rr);
+            for (int rr = 0; rr < LT; ++rr) z[rr] = src_sample_t<I16>(a.iq, a.iq16, x0 + t + (long)T * rr);
             const double slope0 = -2.0 * M_PI * cfo - phi[0] / N;
             double sn, cs, ws, wc;
             sincos(slope0 * (double)t, &sn, &cs);

@@ -1201,6 +1201,7 @@ struct SyncLds {
 // frame's ramp / channel table (ofdm_rx2.hpp rt_size) to rt, in LDS over the
 // stage's small arrays; returns after a barrier. load_tw: fill the twiddle
 // tables here (else they are resident and visible).
+template <bool I16>
 __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsArgs& a, long f, const SyncLds& Ls,
                                            double2* rt, bool load_tw)
 {
@@ -1236,12 +1237,7 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const long j = x0 + (long)G * (tt + 16 * i) + g;
-            if (c.x16) {
-                const short2 q0 = c.x16[j];
-                v[i] = make_double2((double)q0.x, (double)q0.y);
-            } else {
-                v[i] = c.x[j];
-            }
+            v[i] = src_sample_t<I16>(c.x, c.x16, j);
         }
         if (load_tw) {
             load_twiddles<LOGM>(c.tw_sub, tw7, tid, 128);
@@ -1401,7 +1397,7 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
         double2 z[RMAX];
 #pragma unroll
         for (int r = 0; r < RMAX; ++r)
-            z[r] = r < LT ? src_sample(a.iq, a.iq16, x0 + t + (long)T * r) : make_double2(0.0, 0.0);
+            z[r] = r < LT ? src_sample_t<I16>(a.iq, a.iq16, x0 + t + (long)T * r) : make_double2(0.0, 0.0);
         double rs, rc;
         sincospi(-2.0 * cfo * (double)N, &rs, &rc);
         {
@@ -1540,8 +1536,8 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
 #pragma unroll 2
             for (int j = t; j < a.cp; j += T) {
                 const long i0 = x0 + (long)q * L + j, i1 = two ? i0 + L : i0;
-                const double2 a0 = src_sample(a.iq, a.iq16, i0), b0 = src_sample(a.iq, a.iq16, i0 + N);
-                const double2 a1 = src_sample(a.iq, a.iq16, i1), b1 = src_sample(a.iq, a.iq16, i1 + N);
+                const double2 a0 = src_sample_t<I16>(a.iq, a.iq16, i0), b0 = src_sample_t<I16>(a.iq, a.iq16, i0 + N);
+                const double2 a1 = src_sample_t<I16>(a.iq, a.iq16, i1), b1 = src_sample_t<I16>(a.iq, a.iq16, i1 + N);
                 acc0 = cadd(acc0, cconj_mul(a0, b0));
                 acc1 = cadd(acc1, cconj_mul(a1, b1));
             }
@@ -1666,7 +1662,7 @@ __global__ void __launch_bounds__(128, 4) stream_decode_kernel(CfoArgs c, Stream
     // rx stage of the CU's other frames (priority 1 vs 0: 498 -> 478 us;
     // 2 and 3 gain less)
     __builtin_amdgcn_s_setprio(1);
-    sync_frame(c, a, f, Ls, rt, true);
+    sync_frame<I16>(c, a, f, Ls, rt, true);
     __builtin_amdgcn_s_setprio(0);
     rx2_frame<I16, true>(r, f, Lr, reinterpret_cast<const double*>(rt), pk, pbin);
 }
@@ -1694,6 +1690,11 @@ hipError_t launch_stream_decode(const CfoArgs& c, const StreamParamsArgs& a, con
 {
     if (a.nframes <= 0) return hipSuccess;
     if (!r.chan_recip || r.D != a.D || r.S != a.S || r.P != a.P) return hipErrorNotSupported;
+    // the fused kernels are instantiated per stream format (the sample loads
+    // carry no per-sample branch): every view of the stream is the same one
+    const bool i16 = r.iq16 != nullptr;
+    if (i16 != (a.iq16 != nullptr) || i16 != (c.x16 != nullptr) || (!i16 && (!r.iq || !a.iq || !c.x)))
+        return hipErrorInvalidValue;
     // N = 2048 / 4096 with cp = N/4 (configs B, C): ofdm_stream_wide.hip
     if (stream_decode_wide_fits(a, logn, logm, g, c.P)) return launch_stream_decode_wide(c, a, r, logn, st);
     if (!stream_sync_geometry(c, a, logn, logm, g))

@@ -144,5 +144,19 @@ __device__ __forceinline__ double2 src_sample(const double2* iq, const short2* i
     return iq[j];
 }
 
+// src_sample with the stream's format fixed at compile time (kernels
+// instantiated per format): no per-sample branch between the loads, so an
+// unrolled loop issues its loads back to back.
+template <bool I16>
+__device__ __forceinline__ double2 src_sample_t(const double2* iq, const short2* iq16, long j)
+{
+    if constexpr (I16) {
+        const short2 w = iq16[j];
+        return make_double2((double)w.x, (double)w.y);
+    } else {
+        return iq[j];
+    }
+}
+
 }  // namespace
 }  // namespace ofdm
