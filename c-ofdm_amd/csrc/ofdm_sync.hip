@@ -1729,13 +1729,25 @@ struct WalkShape {
     static constexpr int G = WT / T;              // T2 blocks per scan step
 };
 
+// Stream format of the walker's loads: FMT_ANY tests the int16 pointer at
+// run time (one kernel for both formats); FMT_I16 / FMT_F64 fix it at compile
+// time (the walker is instantiated per format: no dead path's registers and
+// no branch between a batch's loads and their uses).
+enum { FMT_ANY = 0, FMT_I16 = 1, FMT_F64 = 2 };
+
+template <int F, class A>
+__device__ __forceinline__ bool fmt_i16(const A& a)
+{
+    return F == FMT_ANY ? a.iq16 != nullptr : F == FMT_I16;
+}
+
 // Stream sample j as complex<double> (int16 wire samples convert exactly, as
 // FRAME_FORM::form_int16_to_double, Frame.hpp:472-481); zero outside [0, n).
-template <class A>
+template <int F = FMT_ANY, class A>
 __device__ __forceinline__ double2 stream_sample(const A& a, long j)
 {
     if (j < 0 || j >= a.n) return make_double2(0.0, 0.0);
-    if (a.iq16) {
+    if (fmt_i16<F>(a)) {
         const short2 v = a.iq16[j];
         return make_double2((double)v.x, (double)v.y);
     }
@@ -1743,10 +1755,10 @@ __device__ __forceinline__ double2 stream_sample(const A& a, long j)
 }
 
 // The same for j known to lie in [0, n) (no per-sample 64-bit bounds test).
-template <class A>
+template <int F = FMT_ANY, class A>
 __device__ __forceinline__ double2 stream_sample_in(const A& a, long j)
 {
-    if (a.iq16) {
+    if (fmt_i16<F>(a)) {
         const short2 v = a.iq16[j];
         return make_double2((double)v.x, (double)v.y);
     }
@@ -1757,7 +1769,7 @@ __device__ __forceinline__ double2 stream_sample_in(const A& a, long j)
 // index is outside [0, n)), all eight loads issued before any is used:
 // clamped addresses and selects, no per-sample branch (a branch around each
 // load, or a use inside it, makes each load wait for the one before).
-template <class A>
+template <int F = FMT_ANY, class A>
 __device__ __forceinline__ void load8_window(const A& a, long base, int lane, int W, double2 (&v)[8])
 {
     long j[8];
@@ -1768,7 +1780,7 @@ __device__ __forceinline__ void load8_window(const A& a, long base, int lane, in
         ok[i] = lane + 64 * i < W && q >= 0 && q < a.n;
         j[i] = ok[i] ? q : 0;
     }
-    if (a.iq16) {  // uniform
+    if (fmt_i16<F>(a)) {  // uniform
         const int* p = reinterpret_cast<const int*>(a.iq16);
         int w[8];
 #pragma unroll
@@ -1788,11 +1800,11 @@ __device__ __forceinline__ void load8_window(const A& a, long base, int lane, in
 
 // x[base + T*i], i < 8, all in [0, n) when `live` (else zeros), loads
 // issued together (the int16 loads waited one by one behind per-sample branches).
-template <int T, class A>
+template <int T, int F = FMT_ANY, class A>
 __device__ __forceinline__ void load8_block(const A& a, long base, bool live, double2 (&v)[8])
 {
     const long b0 = live ? base : 0;
-    if (a.iq16) {  // uniform
+    if (fmt_i16<F>(a)) {  // uniform
         const int* p = reinterpret_cast<const int*>(a.iq16) + b0;
         int w[8];
 #pragma unroll
@@ -1815,21 +1827,21 @@ __device__ __forceinline__ void load8_block(const A& a, long base, bool live, do
 // mode: rx.cpp's zero header before the first SDR buffer, the zeros after a
 // capture): samples outside [0, n) read as zero. Rare (a walk's first and
 // last blocks), so per-sample guards are fine here.
-template <int T, class A>
+template <int T, int F = FMT_ANY, class A>
 __device__ __forceinline__ void load8_block_part(const A& a, long base, double2 (&v)[8])
 {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = stream_sample(a, base + T * i);
+    for (int i = 0; i < 8; ++i) v[i] = stream_sample<F>(a, base + T * i);
 }
 
 __device__ __forceinline__ double energy_rn(double2 v) { return add_rn(mul_rn(v.x, v.x), mul_rn(v.y, v.y)); }
 
 // load8_block rounded to FP32 (int16 wire samples convert exactly).
-template <int T, class A>
+template <int T, int F = FMT_ANY, class A>
 __device__ __forceinline__ void load8_block32(const A& a, long base, bool live, float2 (&v)[8])
 {
     const long b0 = live ? base : 0;
-    if (a.iq16) {  // uniform
+    if (fmt_i16<F>(a)) {  // uniform
         const int* p = reinterpret_cast<const int*>(a.iq16) + b0;
         int w[8];
 #pragma unroll
@@ -1853,12 +1865,12 @@ __device__ __forceinline__ void load8_block32(const A& a, long base, bool live, 
 // (+ new, then - old, separately rounded; each sample's energy as re*re+im*im
 // rounded as the reference rounds it); lags are tested WT at a time with an
 // early exit. xs: C + L samples, normv: C running energies (LDS).
-template <int WT>
+template <int WT, int F>
 __device__ int walk_preamble_exact(const WalkArgs& a, long s, double2* xs, const double2* c, double* normv,
                                    int* best, int t)
 {
     const int L = a.L, C = a.cycles;
-    for (int i = t; i < C + L; i += WT) xs[i] = stream_sample(a, s + i);
+    for (int i = t; i < C + L; i += WT) xs[i] = stream_sample<F>(a, s + i);
     if (t == 0) *best = INT_MAX;
     __syncthreads();
     if (t == 0) {
@@ -1902,17 +1914,17 @@ __device__ int walk_preamble_exact(const WalkArgs& a, long s, double2* xs, const
 // otherwise (margins ~1e-13, practically never) the exact serial search runs.
 // xs: C + L samples, E: C + L energies, normv: C, c: the L template taps
 // (all in the search scratch; c is loaded here).
-template <int WT>
+template <int WT, int F>
 __device__ int walk_preamble(const WalkArgs& a, long s, double2* xs, double2* c, double* E, double* normv,
                              int* best, int* unsure, double* mred, int t)
 {
     constexpr double U = 0x1.0p-53;
     const int L = a.L, C = a.cycles;
-    if (a.exact_only) return walk_preamble_exact<WT>(a, s, xs, a.templ, normv, best, t);
+    if (a.exact_only) return walk_preamble_exact<WT, F>(a, s, xs, a.templ, normv, best, t);
     for (int i = t; i < L; i += WT) c[i] = a.templ[i];
     double emax = 0.0;
     for (int i = t; i < C + L; i += WT) {
-        const double2 v = stream_sample(a, s + i);
+        const double2 v = stream_sample<F>(a, s + i);
         xs[i] = v;
         const double e2 = add_rn(mul_rn(v.x, v.x), mul_rn(v.y, v.y));
         E[i] = e2;
@@ -1981,7 +1993,7 @@ __device__ int walk_preamble(const WalkArgs& a, long s, double2* xs, double2* c,
         const int un = *unsure;
         if (found != INT_MAX) {  // uniform
             __syncthreads();     // every thread has read best/unsure
-            if (un == found) return walk_preamble_exact<WT>(a, s, xs, c, normv, best, t);
+            if (un == found) return walk_preamble_exact<WT, F>(a, s, xs, c, normv, best, t);
             return found;
         }
     }
@@ -2007,7 +2019,7 @@ __device__ int walk_preamble(const WalkArgs& a, long s, double2* xs, double2* c,
 // certain FAIL must be a certain PASS, else the exact search runs. The other
 // waves wait at the closing barrier (the transforms synchronise within the
 // wave only). buf: M entries, P: M doubles (both in the search scratch).
-template <int WT>
+template <int WT, int F>
 __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double* P, const double2* tw_m, int* res,
                                  double2* xs, double* normv, int* best, int t)
 {
@@ -2029,7 +2041,7 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
             const int nl = min(Q, C - i0), W = nl + L - 1;
             const long s0 = s + i0;
             double2 v[8];
-            load8_window(a, s0, lane, W, v);
+            load8_window<F>(a, s0, lane, W, v);
             double emax = 0.0;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
@@ -2129,7 +2141,7 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
     const int found = *res;
     if (found < -1) {  // uniform: a lag within the error bounds of a threshold
         lds_barrier();  // every wave has read *res (the exact search reuses the scratch)
-        return walk_preamble_exact<WT>(a, s, xs, a.templ, normv, best, t);
+        return walk_preamble_exact<WT, F>(a, s, xs, a.templ, normv, best, t);
     }
     return found;
 }
@@ -2156,10 +2168,11 @@ struct WalkLds {
     }
 };
 
-template <int LOGT>
+template <int LOGT, bool I16>
 __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(WalkArgs a)
 {
     constexpr int N = 1 << LOGT, T = N / 8, WT = WalkShape<LOGT>::WT, G = WalkShape<LOGT>::G;
+    constexpr int F = I16 ? FMT_I16 : FMT_F64;
     constexpr int NW = T >= 64 ? T / 64 : 1;  // waves per transform
     // LDS: the T2 transforms and the preamble search run one after the other,
     // so their buffers alias (walk_lds_big): 4 walkers fit a CU
@@ -2294,9 +2307,9 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
             const bool live = ring ? (b + N <= rend && b < a.n) : b + N <= a.n;
             double2 v[8];
             if (ring && live && (b < 0 || b + N > a.n))
-                load8_block_part<T>(a, b + tt, v);
+                load8_block_part<T, F>(a, b + tt, v);
             else
-                load8_block<T>(a, b + tt, live, v);
+                load8_block<T, F>(a, b + tt, live, v);
             // the last pass stays in registers: v[i] = X[tt + T*i], the bins
             // this thread sums (no final LDS write, barrier and re-read); a
             // transform of T <= 64 threads lies within one wave, so its LDS
@@ -2396,16 +2409,16 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
                         if (ring && ((liveA && (bA < 0 || bA + N > a.n)) || (liveB && (bB < 0 || bB + N > a.n)))) {
                             // a block straddles the stream's ends (rare): guarded loads
                             double2 da[8], db[8];
-                            load8_block_part<T>(a, bA + tt, da);
-                            load8_block_part<T>(a, bB + tt, db);
+                            load8_block_part<T, F>(a, bA + tt, da);
+                            load8_block_part<T, F>(a, bB + tt, db);
 #pragma unroll
                             for (int i = 0; i < 8; ++i) {
                                 va[i] = liveA ? make_float2((float)da[i].x, (float)da[i].y) : make_float2(0.f, 0.f);
                                 vb[i] = liveB ? make_float2((float)db[i].x, (float)db[i].y) : make_float2(0.f, 0.f);
                             }
                         } else {
-                            load8_block32<T>(a, bA + tt, liveA, va);
-                            load8_block32<T>(a, bB + tt, liveB, vb);
+                            load8_block32<T, F>(a, bA + tt, liveA, va);
+                            load8_block32<T, F>(a, bB + tt, liveB, vb);
                         }
 #pragma unroll
                         for (int i = 0; i < 8; ++i) v[i] = make_float4(va[i].x, va[i].y, vb[i].x, vb[i].y);
@@ -2494,9 +2507,9 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
         }
         if (ring && hit >= rend - a.out_len) rend += a.ring;  // rx.cpp:147-156: carry, next buffer
         const int lag = (a.tspec && !a.exact_only)
-                            ? walk_preamble_fft<WT>(a, hit, big, P, tw_m, reinterpret_cast<int*>(scr + 2), xs, normv,
+                            ? walk_preamble_fft<WT, F>(a, hit, big, P, tw_m, reinterpret_cast<int*>(scr + 2), xs, normv,
                                                     best, t)
-                            : walk_preamble<WT>(a, hit, xs, ctap, E, normv, best, unsure, mred, t);
+                            : walk_preamble<WT, F>(a, hit, xs, ctap, E, normv, best, unsure, mred, t);
         const long pb = (lag == INT_MAX ? -10 : hit + lag) + 1;  // rx.cpp:160
         if (pb < -2) {                                            // rx.cpp:162-168
             pos = hit + a.msg;
@@ -2559,8 +2572,16 @@ static hipError_t walk_launch_n(const WalkArgs& a, long nblocks, hipStream_t st)
 {
     const size_t shm = walk_shm<LOGT>(a.L, a.cycles, a.tspec != nullptr);
     if (shm > 160 * 1024) return hipErrorInvalidValue;
-    lds_opt_in((const void*)stream_walk_kernel<LOGT>, 160 * 1024);
-    hipLaunchKernelGGL(stream_walk_kernel<LOGT>, dim3((unsigned)nblocks), dim3(WalkShape<LOGT>::WT), shm, st, a);
+    if ((a.iq16 != nullptr) == (a.iq != nullptr)) return hipErrorInvalidValue;  // exactly one stream format
+    if (a.iq16) {
+        lds_opt_in((const void*)stream_walk_kernel<LOGT, true>, 160 * 1024);
+        hipLaunchKernelGGL((stream_walk_kernel<LOGT, true>), dim3((unsigned)nblocks), dim3(WalkShape<LOGT>::WT), shm,
+                           st, a);
+    } else {
+        lds_opt_in((const void*)stream_walk_kernel<LOGT, false>, 160 * 1024);
+        hipLaunchKernelGGL((stream_walk_kernel<LOGT, false>), dim3((unsigned)nblocks), dim3(WalkShape<LOGT>::WT), shm,
+                           st, a);
+    }
     return hipGetLastError();
 }
 
@@ -2575,11 +2596,17 @@ static long walk_slots_n(int L, int C, bool fft)
     long* q = cache[dev];
     if (q[3] && q[0] == L && q[1] == C && q[2] == (long)fft) return q[3];
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
-    lds_opt_in((const void*)stream_walk_kernel<LOGT>, 160 * 1024);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)stream_walk_kernel<LOGT>, WalkShape<LOGT>::WT,
-                                                     walk_shm<LOGT>(L, C, fft)) != hipSuccess ||
-        per <= 0)
-        per = 1;
+    // the fewer resident walkers of the two format instantiations: the
+    // chunking does not depend on the stream's format
+    for (const void* k : {(const void*)stream_walk_kernel<LOGT, false>, (const void*)stream_walk_kernel<LOGT, true>}) {
+        int pk = 0;
+        lds_opt_in(k, 160 * 1024);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&pk, k, WalkShape<LOGT>::WT, walk_shm<LOGT>(L, C, fft)) !=
+                hipSuccess ||
+            pk <= 0)
+            pk = 1;
+        per = per ? std::min(per, pk) : pk;
+    }
     q[0] = L;
     q[1] = C;
     q[2] = fft;
