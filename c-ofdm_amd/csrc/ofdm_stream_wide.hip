@@ -475,9 +475,18 @@ __global__ void __launch_bounds__(WideGeo<LOGN>::NT, 4) stream_decode_wide_kerne
 #pragma unroll
             for (int i = 0; i < 8; ++i) v[i] = make_double2(0.0, 0.0);
         }
-        fft_block_active<LOGN, -1>(v, lq, tw, img, live);
+        // opaque per-symbol copies of the thread index and the carrier slots:
+        // the transform's pass addresses and the gathers are recomputed per
+        // symbol instead of being hoisted out of the loop and spilled (the
+        // loop-invariant addresses went to scratch and came back on every
+        // pass's critical path)
+        int tl;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(tl) : "v"(lq));
+#pragma unroll
+        for (int i = 0; i < RX_DPT; ++i) asm volatile("" : "+v"(pk[i]));
+        fft_block_active<LOGN, -1>(v, tl, tw, img, live);
         if (live) {
-            if (lq < P) pil[s * P + lq] = img[pbin];
+            if (tl < P) pil[s * P + tl] = img[pbin];
 #pragma unroll
             for (int i = 0; i < RX_DPT; ++i) y[q][i] = img[pk[i] & 0xffff];
         }

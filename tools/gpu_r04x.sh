@@ -1,12 +1,14 @@
 #!/bin/bash
-# round 4 (x): wide decode CP sums on every wave (one batch of loads per symbol
-# beside the CFO transform's) against the product build, same box
+# round 4 (x): wide decode variants (V=name: abtest/libofdm_$V.so) against the
+# product build, same box (x: CP sums on every wave; y: opaque per-symbol index, no spills)
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 V=${V:-cp}
-OFDM_MI355X_LIB=$R/abtest/libofdm_$V.so timeout -k 10 300 python -u -m pytest tests/test_gpu_stream.py -k "wide or config_b" -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r04x_tests.log 2>&1 || { tail -30 gpurun_out/r04x_tests.log; exit 1; }
-echo "tests: $(tail -1 gpurun_out/r04x_tests.log)"
+for v in $V; do
+  OFDM_MI355X_LIB=$R/abtest/libofdm_$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_stream.py -k "wide or config_b" -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r04x_tests.log 2>&1 || { tail -30 gpurun_out/r04x_tests.log; exit 1; }
+  echo "$v tests: $(tail -1 gpurun_out/r04x_tests.log)"
+done
 OUT=gpurun_out/r04x_wide_ab.txt; : > $OUT
 for round in 1 2 3; do
   for v in base $V; do
