@@ -278,7 +278,10 @@ int ofdm_preamble_corr(ofdm_ctx* ctx, const double* iq, size_t n, long start, do
 
 /* OFDM_FORM::pilot_freq_sinh (Frame.hpp:285-337): coarse CFO (cycles/sample)
  * of each frame's form from the pilot peaks of its (N+cp)*nsym-point FFT.
- * Needs (N+cp)*nsym = 2^a or 5*2^a. */
+ * Needs (N+cp)*nsym = 2^a or 5*2^a. cfo_out may be pinned host memory
+ * (ofdm_host_alloc): each value is written with a system-scope fence, so a
+ * caller can poll it instead of synchronising the stream (as ofdm_t2_scan's
+ * first_out). */
 int ofdm_cfo_estimate(ofdm_ctx* ctx, const double* x, size_t nframes, size_t frame_stride,
                       int nsym, double* cfo_out, void* stream);
 
