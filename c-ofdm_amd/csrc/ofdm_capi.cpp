@@ -1201,6 +1201,7 @@ int ofdm_cfo_estimate(ofdm_ctx* c, const double* x, size_t nframes, size_t strid
     a.borders = pl->borders;
     a.P = c->P;
     a.cfo_out = cfo_out;
+    a.host_out = 1;  // the public entry: cfo_out may be pinned host memory (header)
     hipError_t e = ofdm::launch_cfo(pl->logm, pl->g, a, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "cfo launch");
     return OFDM_OK;

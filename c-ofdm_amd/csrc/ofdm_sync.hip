@@ -513,7 +513,7 @@ __global__ void __launch_bounds__(G * (1 << LOGM) / 8) cfo_kernel(CfoArgs a)
         shift -= S / 2;
         shift /= S;
         a.cfo_out[f] = shift;
-        __threadfence_system();  // cfo_out may be a pinned host word its caller polls
+        if (a.host_out) __threadfence_system();  // a pinned host word its caller polls
     }
 }
 

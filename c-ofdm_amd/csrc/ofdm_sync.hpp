@@ -45,6 +45,7 @@ struct CfoArgs {
     int P;
     double* cfo_out;
     const long* count;       // nullable: frames beyond min(*count, nframes) are skipped (speculative stream decode)
+    int host_out;            // cfo_out may be pinned host memory: fence each store system-wide (ofdm_cfo_estimate)
 };
 
 struct ShiftArgs {
