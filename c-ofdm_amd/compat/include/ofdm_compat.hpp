@@ -130,7 +130,8 @@ struct Chain {
     // the states after freq_shift / cp / phase (pinned), results, events
     char* hstate[3] = {};
     char *dchan = nullptr, *hchan = nullptr, *hcons = nullptr;  // hcons: the message transform (FFT_FORM::read)
-    double *dcfo = nullptr, *hcfo = nullptr;
+    double *dcfo = nullptr, *hcfo = nullptr;  // hcfo: two pinned words, frames alternate (cfo_slot)
+    int cfo_slot = 0;
     // Modulation::demod of the channel-divided message (rx.cpp:211-220): the
     // points and their decisions, written by the rx kernel to pinned memory
     char* hcons_eq = nullptr;

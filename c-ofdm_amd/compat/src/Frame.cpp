@@ -413,11 +413,17 @@ double OFDM_FORM::pilot_freq_sinh()
         const DevRange r = stage_in(*ctx_, 1, ch->region, ch->region_bytes);
         void* st = e.stream;
         // the estimate lands straight in its pinned word (no copy launch);
-        // the chain below reads it from there, and the host polls it
-        volatile double* hc = ch->hcfo;
+        // the chain below reads it from there, and the host polls it. Frames
+        // alternate between two words: the previous frame's chain may still
+        // be queued behind its estimate (which this host thread has seen) and
+        // read its word, while this frame's is reset here; the one before it
+        // ran ahead of that estimate in stream order.
+        ch->cfo_slot ^= 1;
+        double* wc = ch->hcfo + ch->cfo_slot;
+        volatile double* hc = wc;
         const uint64_t unset = 0x7ff4dead0badf00dull;  // a NaN the estimate never is
         std::memcpy(const_cast<double*>(hc), &unset, sizeof(unset));
-        check(ofdm_cfo_estimate(ctx_->ctx, (const double*)r.d, 1, (size_t)size, num_symb, ch->hcfo, st),
+        check(ofdm_cfo_estimate(ctx_->ctx, (const double*)r.d, 1, (size_t)size, num_symb, wc, st),
               "ofdm_cfo_estimate");
         check(ofdm_event_record(e.ctx, ch->ev[0], st), "ofdm_event_record");
         // the chain runs in place on the frame's device image: it is marked
@@ -430,7 +436,7 @@ double OFDM_FORM::pilot_freq_sinh()
         r.m->stale_hi = r.m->stale_lo + ch->region_bytes;
         // main.cpp:61-63 in one launch, each state written straight into its
         // pinned copy (what output[0] holds after each member)
-        check(ofdm_sync_chain(mw, (double*)dr, 1, nw, nw, nsym, ch->hcfo, (double*)ch->hstate[0],
+        check(ofdm_sync_chain(mw, (double*)dr, 1, nw, nw, nsym, wc, (double*)ch->hstate[0],
                               (double*)ch->hstate[1], (double*)ch->hstate[2], 0, st),
               "ofdm_sync_chain");
         check(ofdm_event_record(e.ctx, ch->ev[3], st), "ofdm_event_record");

@@ -365,7 +365,7 @@ bool Chain::alloc(Engine& e)
     hchan = static_cast<char*>(p);
     check(ofdm_host_alloc(c, cons_bytes, &p), "ofdm_host_alloc");
     hcons = static_cast<char*>(p);
-    check(ofdm_host_alloc(c, sizeof(double), &p), "ofdm_host_alloc");
+    check(ofdm_host_alloc(c, 2 * sizeof(double), &p), "ofdm_host_alloc");
     hcfo = static_cast<double*>(p);
     check(ofdm_host_alloc(c, cons_bytes, &p), "ofdm_host_alloc");
     hcons_eq = static_cast<char*>(p);
