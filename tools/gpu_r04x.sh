@@ -13,7 +13,7 @@ OUT=gpurun_out/r04x_wide_ab.txt; : > $OUT
 for round in 1 2 3; do
   for v in base $V; do
     if [ $v = base ]; then unset OFDM_MI355X_LIB; else export OFDM_MI355X_LIB=$R/abtest/libofdm_$v.so; fi
-    for args in "--config B --frames 4096" "--config B --frames 4096 --i16" "--config C --frames 2048"; do
+    for args in "--config B --frames 4096" "--config B --frames 4096 --i16"; do
       D=$R/gpurun_out/ab_prof; rm -rf $D
       timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- python3 tools/stream_bench.py --reps 5 $args > gpurun_out/ab_sb.log 2>&1 || { tail gpurun_out/ab_sb.log; exit 1; }
       python3 - "$v" "$args" "$D/run_kernel_stats.csv" gpurun_out/ab_sb.log >> $OUT <<'PY'
