@@ -2106,7 +2106,7 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
             const double Mall = (mrun + erun) * 1.0625;
             const double scan_err = (4.0 * R + 64.0) * U * ptot;
             const double ef = 1024.0 * U * sqrt(ptot * 1.0625) * a.tspec_max;
-#pragma unroll 2
+#pragma unroll 1  // rolled: it exits at the first decided lag
             for (int j = 0; j < 8; ++j) {
                 const int r = lane + 64 * j, i = i0 + r;
                 int d = 0;  // 0 = certain FAIL, 1 = certain PASS, 2 = uncertain
