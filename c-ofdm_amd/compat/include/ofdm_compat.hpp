@@ -32,7 +32,9 @@ struct Engine {
     void* stream = nullptr;
     char* arena = nullptr;
     size_t arena_bytes = 0, arena_used = 0;
+    int* t2_word = nullptr;   // pinned: find_t2sin's answer, written by the detector's last workgroup
     void* stage(size_t bytes);                                // arena slice (synchronises when full)
+    volatile int* t2_answer();                                // t2_word (allocated on first use)
     void h2d(void* dev, const void* host, size_t bytes);      // staged, asynchronous
     void h2d_pinned(void* dev, const void* pinned, size_t bytes);
     void d2h(void* host, const void* dev, size_t bytes);      // synchronous
@@ -130,7 +132,7 @@ struct Chain {
     // the states after freq_shift / cp / phase (pinned), results, events
     char* hstate[3] = {};
     char *dchan = nullptr, *hchan = nullptr, *hcons = nullptr;  // hcons: the message transform (FFT_FORM::read)
-    double *dcfo = nullptr, *hcfo = nullptr;  // hcfo: two pinned words, frames alternate (cfo_slot)
+    double* hcfo = nullptr;  // two pinned words the CFO kernel writes, frames alternate (cfo_slot)
     int cfo_slot = 0;
     // Modulation::demod of the channel-divided message (rx.cpp:211-220): the
     // points and their decisions, written by the rx kernel to pinned memory

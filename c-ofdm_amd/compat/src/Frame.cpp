@@ -253,11 +253,12 @@ int T2SIN_FORM::find_t2sin(complex_vector& signal, int start_index)
         const long nb = std::min(w, nblocks - b0);
         const size_t len = (size_t)nb * size;
         const DevRange x = stage_in(*ctx_, 0, signal.data() + start_index + b0 * size, len * CD);
-        // the launch's last workgroup writes the answer straight to a pinned
-        // word (no copy launch, no stream synchronisation): poll it. The
-        // detector's tail may still retire when this returns; the next call
-        // on the thread's stream is ordered after it.
-        volatile int* hf = static_cast<volatile int*>(ctx_->engine().stage(sizeof(int)));
+        // the launch's last workgroup writes the answer straight to the
+        // engine's pinned word (no copy launch, no stream synchronisation):
+        // poll it. The detector's tail may still retire when this returns
+        // (it writes the word once, before that); the next call on the
+        // thread's stream is ordered after it.
+        volatile int* hf = ctx_->engine().t2_answer();
         *hf = INT_MIN;
         check(ofdm_t2_scan(ctx_->ctx, (const double*)x.d, len, 0, nullptr, const_cast<int*>(hf), ctx_->stream()),
               "ofdm_t2_scan");

@@ -155,6 +155,16 @@ void* Engine::stage(size_t bytes)
     return p;
 }
 
+volatile int* Engine::t2_answer()
+{
+    if (!t2_word) {
+        void* h = nullptr;
+        check(ofdm_host_alloc(ctx, sizeof(int), &h), "ofdm_host_alloc");
+        t2_word = static_cast<int*>(h);
+    }
+    return t2_word;
+}
+
 void Engine::h2d(void* dev, const void* host, size_t bytes)
 {
     if (!bytes) return;
@@ -340,8 +350,7 @@ Chain::~Chain()
     for (int i = 0; i < 3; ++i) {
         if (hstate[i]) ofdm_host_free(c, hstate[i]);
     }
-    for (void* d : {(void*)dchan, (void*)dcfo})
-        if (d) ofdm_device_free(c, d);
+    if (dchan) ofdm_device_free(c, dchan);
     for (void* h : {(void*)hchan, (void*)hcons, (void*)hcfo, (void*)hcons_eq, (void*)hbits})
         if (h) ofdm_host_free(c, h);
     for (void* e : ev)
@@ -351,7 +360,7 @@ Chain::~Chain()
 bool Chain::alloc(Engine& e)
 {
     (void)e;
-    if (dcfo) return true;
+    if (hcfo) return true;
     if (!mwp_ctx || !region) return false;
     ofdm_ctx* c = mwp_ctx->ctx;
     void* p = nullptr;
@@ -365,8 +374,6 @@ bool Chain::alloc(Engine& e)
     hchan = static_cast<char*>(p);
     check(ofdm_host_alloc(c, cons_bytes, &p), "ofdm_host_alloc");
     hcons = static_cast<char*>(p);
-    check(ofdm_host_alloc(c, 2 * sizeof(double), &p), "ofdm_host_alloc");
-    hcfo = static_cast<double*>(p);
     check(ofdm_host_alloc(c, cons_bytes, &p), "ofdm_host_alloc");
     hcons_eq = static_cast<char*>(p);
     bits_bytes = (size_t)msg_ctx->geo.bytes_per_frame;
@@ -374,8 +381,8 @@ bool Chain::alloc(Engine& e)
     check(ofdm_host_alloc(c, bits_bytes, &p), "ofdm_host_alloc");
     hbits = static_cast<uint8_t*>(p);
     for (auto& v : ev) check(ofdm_event_create(c, &v), "ofdm_event_create");
-    check(ofdm_device_alloc(c, sizeof(double), &p), "ofdm_device_alloc");
-    dcfo = static_cast<double*>(p);
+    check(ofdm_host_alloc(c, 2 * sizeof(double), &p), "ofdm_host_alloc");
+    hcfo = static_cast<double*>(p);  // last: the allocation marker
     return true;
 }
 

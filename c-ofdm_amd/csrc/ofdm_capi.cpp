@@ -180,6 +180,11 @@ struct ofdm_ctx {
     hipEvent_t ev_walk = nullptr;  // walk records landed in h_walk
     hipEvent_t ev_wdone = nullptr;  // the walk kernel finished (caller's stream)
     hipStream_t side = nullptr;     // copies the walk records out beside the decode
+    // look-back walk: per-chunk publication counts (zero between calls: the
+    // resolve kernel clears them), the true walk's records for shard reports,
+    // and the resolve kernel's status block (page-locked, written by the kernel)
+    Grow s_pub, s_chain, h_status;
+    bool pub_zero = false;         // every s_pub word is zero
 
     ofdm::DevTables tables(bool bpsk) const
     {
@@ -323,9 +328,9 @@ int ofdm_destroy(ofdm_ctx* c)
                     c->d_t2tw, c->d_first, c->d_scratch, c->d_cfo_scratch, c->d_pre_hv, c->d_pre_done};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
-    for (auto* g : {&c->s_walk, &c->s_batch, &c->s_chan, &c->s_pbs})
+    for (auto* g : {&c->s_walk, &c->s_batch, &c->s_chan, &c->s_pbs, &c->s_pub, &c->s_chain})
         if (g->p) (void)hipFree(g->p);
-    for (auto* g : {&c->h_walk, &c->h_frames})
+    for (auto* g : {&c->h_walk, &c->h_frames, &c->h_status})
         if (g->p) (void)hipHostFree(g->p);
     if (c->d_queue) (void)hipFree(c->d_queue);
     if (c->d_rxq) (void)hipFree(c->d_rxq);
@@ -1361,7 +1366,7 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
                           long chunk, long* pb_out, uint8_t* bytes_out, double* constell_out, double* cfo_out,
                           size_t* nframes_out, void* stream, ofdm_walk_state start_state, long own_lo, long own_hi,
                           long* located, uint8_t* located_lag, size_t located_cap, size_t* nlocated_out,
-                          ofdm_walk_state* exit_out)
+                          ofdm_walk_state* exit_out, bool force_halo = false)
 {
     if (!c || (!iq && !iq16) || !nframes_out) return fail(OFDM_ERR_INVALID, "null argument");
     *nframes_out = 0;
@@ -1384,38 +1389,45 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     const long L = c->L, pre = (long)L * c->npr, msg = (long)L * c->S, span = pre + msg;
     const long flen = c->geo.frame_len, nn = (long)n;
     if (nn == 0 || start >= nn) return OFDM_OK;
-    // walkers: one chunk per resident walker slot (a single round: every
-    // chunk re-walks a 3-frame halo to meet the true walk, so fewer, longer
-    // chunks cost less), each >= 8 frames
+    // walkers: one chunk per resident walker slot by default, each >= 8 frames
     const long slots = ofdm::stream_walk_slots(c->t2_logn, (int)c->p.pr_sin_len,
                                                (int)(2 * c->p.t2sin_size + c->p.pr_sin_len), c->d_tspec != nullptr);
     // Per-context tuning (ofdm_set_walk_tuning): chunks per walker slot,
-    // walk-in halo and walk-on extension in 1/1000 frames. Defaults: one
-    // chunk per slot, 3-frame halo, no extension (tools/walk_q_sweep.sh:
-    // 1.5-frame halos with a 2-frame extension, or 2-3 chunks per slot, gain
-    // nothing measurable on config 4; shorter halos force re-walks).
+    // walk-in halo and walk-on extension in 1/1000 frames, look-back
+    // stitching. Look-back (the default): chunks start at their core (no
+    // walk-in) and each walks on past its core end until its walk joins the
+    // next chunk's (a device-side check of the records that chunk publishes);
+    // the chain of joined walks is the sequential walk, resolved on the
+    // device. Without it (lookback = 0, or the fallback when a walker's
+    // records overflow): each chunk walks in from a 3-frame halo and the host
+    // stitches the walks, re-walking a chunk whose walk-in did not meet the
+    // true walk.
     const ofdm_walk_tuning& tu = c->walk;
     const long qper = std::max(1L, tu.chunks_per_slot);
     const long span_w = own_hi - own_lo;  // the chunk cores tile [own_lo, own_hi)
     if (chunk <= 0) chunk = std::max(8 * flen, (span_w + slots * qper - 1) / (slots * qper));
     chunk = std::max(chunk, (long)c->t2);
-    const long halo = std::max(0L, tu.halo_milli) * flen / 1000;
-    const long ext = std::max(0L, tu.ext_milli) * flen / 1000;
     const long nchunks = std::max(1L, (span_w + chunk - 1) / chunk);
     if (nchunks > 1 << 20) return fail(OFDM_ERR_INVALID, "chunk too small for this stream");
+    const bool lbk = tu.lookback && !force_halo && nchunks <= ofdm::RESOLVE_MAX_CHUNKS;
+    const long halo = (tu.halo_milli < 0 ? (lbk ? 0L : 3000L) : tu.halo_milli) * flen / 1000;
+    const long ext = std::max(0L, tu.ext_milli) * flen / 1000;
     // each located frame advances the walk by > message_len, and a walker can
     // walk on past its core end by ext plus one scan step (WALK_SCAN_MAX
     // samples) and the preamble window: this many records always suffice
-    // (chunk 0 walks in from `start`, the others a halo before their core)
+    // (chunk 0 walks in from `start`, the others a halo before their core).
+    // A look-back walker may walk on through the next core too (its walk met
+    // no record of that chunk's); one more overflows: the host falls back
     const int max_rec =
-        (int)((chunk + std::max(halo, own_lo - start) + std::max(ext, 2 * flen) + ofdm::WALK_SCAN_MAX + 2 * c->p.t2sin_size +
-               c->p.pr_sin_len) / msg + 4);
+        (int)(((lbk ? 2 : 1) * chunk + std::max(halo, own_lo - start) + std::max(ext, 2 * flen) + ofdm::WALK_SCAN_MAX +
+               2 * c->p.t2sin_size + c->p.pr_sin_len) / msg + (lbk ? 8 : 4));
     int rc;
     const size_t rec_b = (size_t)nchunks * max_rec * sizeof(long);
     // layout: records | exit states | exit ring ends | re-walk start (pos, ring end) | counts | ...
     const size_t walk_b0 = rec_b + (size_t)nchunks * (2 * sizeof(long) + sizeof(int)) + 2 * sizeof(long) + 64;
     const size_t walk_b = walk_b0 + 2 * (size_t)nchunks * sizeof(int);  // + in-core counts and first indices
-    if ((rc = grow(c, c->s_walk, walk_b))) return rc;
+    const size_t link_b = 3 * (size_t)nchunks * sizeof(int);            // + look-back links
+    if ((rc = grow(c, c->s_walk, walk_b + link_b))) return rc;
     char* wb = static_cast<char*>(c->s_walk.p);
     long* d_rec = reinterpret_cast<long*>(wb);
     long* d_exit = reinterpret_cast<long*>(wb + rec_b);
@@ -1425,6 +1437,7 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     int* d_ids = d_nrec + nchunks;     // one re-walk chunk id (in the 64 B slack)
     int* d_ncore = reinterpret_cast<int*>(wb + walk_b0);
     int* d_first_in = d_ncore + nchunks;
+    int* d_link = reinterpret_cast<int*>(wb + walk_b);
 
     ofdm::WalkArgs w{};
     w.exact_only = tu.exact_search != 0;
@@ -1496,6 +1509,17 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     } call_done{c, st};
     if (!c->queue_zero) HIP_TRY(hipMemsetAsync(w.queue, 0, sizeof(int), st));
     c->queue_zero = false;
+    if (lbk) {
+        if (c->s_pub.bytes < (size_t)nchunks * sizeof(int)) {
+            if ((rc = grow(c, c->s_pub, (size_t)std::max(nchunks, 2048L) * sizeof(int)))) return rc;
+            c->pub_zero = false;
+        }
+        if (!c->pub_zero) HIP_TRY(hipMemsetAsync(c->s_pub.p, 0, c->s_pub.bytes, st));
+        c->pub_zero = false;  // until the resolve kernel clears it again
+        w.lookback = 1;
+        w.pub = static_cast<int*>(c->s_pub.p);
+        w.link = d_link;
+    }
     hipError_t e = ofdm::launch_stream_walk(c->t2_logn, w, std::min(nchunks, slots), st);
     if (e != hipSuccess) return hip_fail(e, "stream_walk launch");
 
@@ -1599,6 +1623,111 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
         }
         return OFDM_OK;
     };
+    // Geometries the fused kernels do not take: gather each frame of d_list
+    // into a batch, then the staged sync chain + demod
+    auto decode_gathered = [&](const long* d_list, size_t nout) -> int {
+        const size_t fb = (size_t)span * sizeof(double2);
+        const size_t bmax = std::max<size_t>(1, std::min<size_t>(65535, ((size_t)256 << 20) / fb));
+        const size_t nb0 = std::min(nout, bmax);
+        int r2;
+        if ((r2 = grow(c, c->s_batch, nb0 * fb)) || (r2 = grow(c, c->s_chan, nb0 * c->D * sizeof(double2)))) return r2;
+        double* batch = static_cast<double*>(c->s_batch.p);
+        double* chan = static_cast<double*>(c->s_chan.p);
+        for (size_t f0 = 0; f0 < nout; f0 += nb0) {
+            const size_t nb = std::min(nb0, nout - f0);
+            ofdm::GatherArgs ga{reinterpret_cast<const double2*>(iq), reinterpret_cast<const short2*>(iq16), nn,
+                                d_list + f0, (long)nb, span, reinterpret_cast<double2*>(batch)};
+            hipError_t e2 = ofdm::launch_gather(ga, st);
+            if (e2 != hipSuccess) return hip_fail(e2, "gather launch");
+            if ((r2 = ofdm_sync_frames(c, batch, nb, (size_t)span, OFDM_SYNC_ALL, nullptr,
+                                       cfo_out ? cfo_out + f0 : nullptr, chan, stream)))
+                return r2;
+            if ((r2 = ofdm_rx_demod(c, batch + 2 * pre, nb, (size_t)span, chan, (size_t)c->D,
+                                    constell_out ? constell_out + 2 * f0 * npts : nullptr,
+                                    bytes_out ? bytes_out + f0 * c->geo.bytes_per_frame : nullptr, nullptr, nullptr,
+                                    stream)))
+                return r2;
+        }
+        return OFDM_OK;
+    };
+
+    if (lbk) {
+        // The true walk, resolved on the device: the owned frames straight
+        // into the decode's list (and pb_out), a status block to the host.
+        // The decode is enqueued behind it before the host reads the status.
+        const size_t ub = std::min(max_frames, (size_t)nchunks * max_rec);
+        const bool want_chain = located || nlocated_out;
+        const size_t chain_cap = want_chain ? (size_t)nchunks * max_rec : 0;
+        if ((rc = grow(c, c->s_pbs, (ub + 1) * sizeof(long))) || (rc = grow_host(c, c->h_status, 64)) ||
+            (want_chain && (rc = grow(c, c->s_chain, chain_cap * sizeof(long)))))
+            return rc;
+        long* d_pbs = static_cast<long*>(c->s_pbs.p);
+        volatile long* hs = static_cast<volatile long*>(c->h_status.p);
+        hs[1] = -1;  // overwritten by the resolve kernel
+        ofdm::ResolveArgs ra{};
+        ra.rec = d_rec;
+        ra.nrec = d_nrec;
+        ra.link = d_link;
+        ra.exit_pos = d_exit;
+        ra.exit_ring = d_exit_ring;
+        ra.nchunks = nchunks;
+        ra.max_rec = max_rec;
+        ra.own_lo = own_lo;
+        ra.own_hi = own_hi;
+        ra.cap = (long)ub;
+        ra.list = d_pbs;
+        ra.list2 = pb_out;
+        ra.count = d_pbs + ub;
+        ra.chain = want_chain ? static_cast<long*>(c->s_chain.p) : nullptr;
+        ra.chain_cap = (long)chain_cap;
+        ra.status = const_cast<long*>(hs);
+        ra.pub = w.pub;
+        ra.queue_reset = c->d_queue;
+        e = ofdm::launch_resolve(ra, st);
+        if (e != hipSuccess) return hip_fail(e, "stream resolve launch");
+        c->pub_zero = true;    // cleared by the resolve (stream order)
+        c->queue_zero = true;  // likewise the chunk counter
+        if (!c->ev_wdone) HIP_TRY(hipEventCreateWithFlags(&c->ev_wdone, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(c->ev_wdone, st));
+        const bool spec = fused && ub > 0 && ub * per <= ((size_t)256 << 20);
+        if (spec && (rc = decode_fused(d_pbs, ub, d_pbs + ub))) return rc;
+        HIP_TRY(hipEventSynchronize(c->ev_wdone));
+        const long owned = hs[0], flags = hs[1], xpos = hs[2], xring = hs[3], nchain = hs[4];
+        if (flags < 0) return fail(OFDM_ERR_HIP, "stream resolve wrote no status");
+        if (flags & ofdm::RESOLVE_OVERFLOW) {
+            // a walker's records overflowed (a walk that met no later chunk's
+            // through a whole core): the halo walk with host stitching
+            if (getenv("OFDM_STREAM_DEBUG")) fprintf(stderr, "ofdm_rx_stream: look-back overflow, halo walk\n");
+            return rx_stream_impl(c, iq, iq16, n, max_frames, chunk, pb_out, bytes_out, constell_out, cfo_out,
+                                  nframes_out, stream, start_state, own_lo, own_hi, located, located_lag, located_cap,
+                                  nlocated_out, exit_out, true);
+        }
+        if (flags & ofdm::RESOLVE_NEG_FRAME)
+            return fail(OFDM_ERR_UNSUPPORTED, "a frame starts before the stream's first sample "
+                                              "(rx.cpp's ring would decode it from its zero header)");
+        *nframes_out = (size_t)owned;
+        if (exit_out) *exit_out = ofdm_walk_state{xpos, xpos < 0 ? 0 : xring};
+        if (want_chain) {
+            if (nlocated_out) *nlocated_out = (size_t)nchain;
+            const size_t nl = std::min({(size_t)nchain, located_cap, chain_cap});
+            if (nl && (located || located_lag)) {
+                std::vector<long> rl(nl);
+                HIP_TRY(hipMemcpy(rl.data(), c->s_chain.p, nl * sizeof(long), hipMemcpyDeviceToHost));
+                for (size_t i = 0; i < nl; ++i) {
+                    const long r = rl[i];
+                    if (located) located[i] = r < 0 ? r : (r & ofdm::WALK_REC_PB);
+                    if (located_lag) located_lag[i] = r > 0 && (r & ofdm::WALK_REC_LAG) ? 1 : 0;
+                }
+            }
+        }
+        if (getenv("OFDM_STREAM_DEBUG"))
+            fprintf(stderr, "ofdm_rx_stream: look-back, %ld chunks of %ld samples, halo %ld, %ld frames\n", nchunks,
+                    chunk, halo, owned);
+        const size_t nout = std::min((size_t)owned, ub);
+        if (spec || nout == 0) return OFDM_OK;
+        if (fused) return decode_fused(d_pbs, nout, nullptr);
+        return decode_gathered(d_pbs, nout);
+    }
 
     // records, exit states and counts in one copy of the walk buffer's layout
     if ((rc = grow_host(c, c->h_walk, walk_b))) return rc;
@@ -1781,30 +1910,7 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     if (pb_out) HIP_TRY(hipMemcpyAsync(pb_out, d_pbs, nout * sizeof(long), hipMemcpyDeviceToDevice, st));
 
     if (fused) return decode_fused(d_pbs, nout, nullptr);
-
-    // Fallback: gather each frame into a batch, then the staged sync chain + demod
-    const size_t fb = (size_t)span * sizeof(double2);
-    const size_t bmax = std::max<size_t>(1, std::min<size_t>(65535, ((size_t)256 << 20) / fb));
-    const size_t nb0 = std::min(nout, bmax);
-    if ((rc = grow(c, c->s_batch, nb0 * fb)) || (rc = grow(c, c->s_chan, nb0 * c->D * sizeof(double2)))) return rc;
-    double* batch = static_cast<double*>(c->s_batch.p);
-    double* chan = static_cast<double*>(c->s_chan.p);
-    for (size_t f0 = 0; f0 < nout; f0 += nb0) {
-        const size_t nb = std::min(nb0, nout - f0);
-        ofdm::GatherArgs ga{reinterpret_cast<const double2*>(iq), reinterpret_cast<const short2*>(iq16), nn,
-                            d_pbs + f0, (long)nb, span, reinterpret_cast<double2*>(batch)};
-        e = ofdm::launch_gather(ga, st);
-        if (e != hipSuccess) return hip_fail(e, "gather launch");
-        if ((rc = ofdm_sync_frames(c, batch, nb, (size_t)span, OFDM_SYNC_ALL, nullptr, cfo_out ? cfo_out + f0 : nullptr,
-                                   chan, stream)))
-            return rc;
-        if ((rc = ofdm_rx_demod(c, batch + 2 * pre, nb, (size_t)span, chan, (size_t)c->D,
-                                constell_out ? constell_out + 2 * f0 * npts : nullptr,
-                                bytes_out ? bytes_out + f0 * c->geo.bytes_per_frame : nullptr, nullptr, nullptr,
-                                stream)))
-            return rc;
-    }
-    return OFDM_OK;
+    return decode_gathered(d_pbs, nout);
 }
 
 extern "C" {
@@ -1840,11 +1946,12 @@ int ofdm_walk_tuning_default(ofdm_walk_tuning* o)
     if (!o) return fail(OFDM_ERR_INVALID, "null argument");
     *o = ofdm_walk_tuning{};
     o->chunks_per_slot = 1;
-    o->halo_milli = 3000;
+    o->halo_milli = -1;
     o->ext_milli = 0;
     o->exact_search = 0;
     o->t2_f32 = 1;
     o->t2_margin = 4e-5;
+    o->lookback = 1;
     return OFDM_OK;
 }
 
@@ -1859,7 +1966,8 @@ int ofdm_set_walk_tuning(ofdm_ctx* c, const ofdm_walk_tuning* t)
 {
     if (!c || !t) return fail(OFDM_ERR_INVALID, "null argument");
     if (t->staged_decode != 0 && t->staged_decode != 1) return fail(OFDM_ERR_INVALID, "staged_decode must be 0 or 1");
-    if (t->chunks_per_slot < 1 || t->halo_milli < 0 || t->ext_milli < 0 || !(t->t2_margin >= 0.0))
+    if (t->lookback != 0 && t->lookback != 1) return fail(OFDM_ERR_INVALID, "lookback must be 0 or 1");
+    if (t->chunks_per_slot < 1 || t->halo_milli < -1 || t->ext_milli < 0 || !(t->t2_margin >= 0.0))
         return fail(OFDM_ERR_INVALID, "walk tuning out of range");
     if (t->t2_margin < 4e-5 && !t->allow_uncertified)
         return fail(OFDM_ERR_INVALID, "t2_margin %g is below the certified 4e-5 (the walk could differ from the "
@@ -1890,8 +1998,11 @@ int ofdm_stream_initial_state(const ofdm_ctx* c, ofdm_walk_state* out)
 int ofdm_set_stream_ring(ofdm_ctx* c, long ring)
 {
     if (!c) return fail(OFDM_ERR_INVALID, "null ctx");
-    if (ring < 0 || (ring > 0 && ring < 2 * c->geo.frame_len))
-        return fail(OFDM_ERR_INVALID, "ring must be 0 or at least 2 * output_size (rx.cpp's buffer holds output_size + R)");
+    // R >= output_size: the smallest ring a config makes (rx_buf_size = 1,
+    // Frame.cpp:221, sdr.hpp:141), the default ofdm_create sets from it
+    if (ring < 0 || (ring > 0 && ring < c->geo.frame_len))
+        return fail(OFDM_ERR_INVALID, "ring must be 0 or at least output_size (rx.cpp's buffer holds output_size + R, "
+                                      "R = rx_buf_size * output_size)");
     c->ring = ring;
     return OFDM_OK;
 }

@@ -132,6 +132,7 @@ __global__ void t2_finalize_kernel(const int* scratch, int* first_out, long star
 {
     const int m = *scratch;
     *first_out = m == INT_MAX ? -1 : (int)(start + (long)m * size);
+    __threadfence_system();  // as t2_scan_kernel: a pinned host answer may be polled by the caller
 }
 
 template <int LOGN>
@@ -2147,6 +2148,35 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
     return found;
 }
 
+// Look-back (WalkArgs::lookback), thread 0 of a walker that located the frame
+// with record r at pb, past its own core end and inside chunk m's core: the
+// index of r in m's published records, or -1 when m's walk does not hold it
+// (m published a record past pb, or finished). While m has not reached pb
+// the walker waits for it, but only once m has been taken from the queue: its
+// walker is then resident, and it publishes every record before any wait of
+// its own, so the wait ends. Records and counts are stored write-through
+// (sc1) by the publishing lane, which drains its stores before each count;
+// every load here is an sc1 load of them.
+__device__ int lookback_find(const WalkArgs& a, long pb, long r)
+{
+    const long m = (pb - a.core_lo) / a.chunk;
+    const long* rm = a.rec + m * a.max_rec;
+    for (int spin = 0;; ++spin) {
+        const int pv = __hip_atomic_load(a.pub + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // the record loads stay behind the poll
+        const int cnt = min(pv & (WALK_PUB_DONE - 1), a.max_rec);
+        for (int j = 0; j < cnt; ++j) {
+            const long v = __hip_atomic_load(rm + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (v == r) return j;
+            if ((v < 0 ? v : (v & WALK_REC_PB)) > pb) return -1;  // m's walk passed pb without this frame
+        }
+        if (pv & WALK_PUB_DONE) return -1;
+        if (spin >= WALK_SPIN_MAX || __hip_atomic_load(a.queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= m)
+            return -1;  // m not taken yet: walk on (always exact), and look again at the next frame
+        __builtin_amdgcn_s_sleep(4);
+    }
+}
+
 }  // namespace
 
 // LDS of a walker: the fixed part, then the scratch (`big`) that the T2
@@ -2234,8 +2264,16 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
         c = a.chunk_ids ? a.chunk_ids[blockIdx.x] : (int)blockIdx.x;
     }
     // chunk cores tile [core_lo, core_hi); chunk 0 walks in from the given
-    // start state, the others from a halo before their core
-    const long core0 = a.core_lo + (long)c * a.chunk, end = min(core0 + a.chunk, a.core_hi);
+    // start state, the others from a halo before their core (look-back: none
+    // by default). `end` is where the walk's exit logic applies: the chunk's
+    // core end, or with look-back core_hi (a chunk walks on past its core
+    // until its walk joins a later chunk's)
+    const bool lb = a.lookback != 0;  // uniform
+    const long core0 = a.core_lo + (long)c * a.chunk, cend = min(core0 + a.chunk, a.core_hi);
+    const long end = lb ? a.core_hi : cend;
+    // look-back link {chunk this walk joins, the shared frame's index here and
+    // there}: none until the walk joins one
+    if (lb && t0 == 0) a.link[3 * c] = -1;
     long pos = a.start_pos ? a.start_pos[blockIdx.x] : (c == 0 ? a.start : (core0 > a.halo ? core0 - a.halo : 0));
     const bool ring = a.ring > 0;  // uniform
     // ring mode: the first ring end after position q (the ring ends lie on
@@ -2280,7 +2318,7 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
             // resident wave, whatever its progress: equal chunks finished in
             // dispatch order (253 us for a CU's first walker, 325 us for its
             // eighth), and the CUs drained slowly (walker 386 -> 365 us)
-            const long left = end - pos, span = end - core0 + a.halo;
+            const long left = cend - pos, span = cend - core0 + a.halo;
             const int pr = left <= 0 ? 0 : (int)min(3L, left * 4 / max(1L, span));
             switch (__builtin_amdgcn_readfirstlane(pr)) {
                 case 3: __builtin_amdgcn_s_setprio(3); break;
@@ -2511,23 +2549,54 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
                             ? walk_preamble_fft<WT, F>(a, hit, big, P, tw_m, reinterpret_cast<int*>(scr + 2), xs, normv,
                                                     best, t)
                             : walk_preamble<WT, F>(a, hit, xs, ctap, E, normv, best, unsure, mred, t);
-        const long pb = (lag == INT_MAX ? -10 : hit + lag) + 1;  // rx.cpp:160
-        if (pb < -2) {                                            // rx.cpp:162-168
+        // rx.cpp:160-168: find_preamble's -10 (no lag passes) moves on by a
+        // message. rx.cpp tests preamble_begin < -2 in buffer coordinates,
+        // where a found preamble gives >= 1; in stream coordinates a found
+        // preamble may lie in the ring's zero header (pb < 0, a capture that
+        // starts inside a frame), so the test is on the search result itself
+        if (lag == INT_MAX) {
             pos = hit + a.msg;
             continue;
         }
+        const long pb = hit + lag + 1;
         if (ring && pb >= rend - a.out_len + N) rend += a.ring;  // rx.cpp:180-189
         if (pb + a.pre + a.msg > a.n) break;  // frame not in the stream: the walk ends
+        // ring mode: the state after the frame, (pb + msg, rend), is one of
+        // two; the record says which (a frame before the stream's first
+        // sample is kept as is: the host rejects it)
+        const long rv = (ring && pb >= 0 && rend != ring_after(pb + a.msg)) ? (pb | WALK_REC_LAG) : pb;
         if (t == 0 && nrec < a.max_rec) {
-            // ring mode: the state after the frame, (pb + msg, rend), is one of
-            // two; the record says which (a frame before the stream's first
-            // sample is kept as is: the host rejects it)
-            const bool lagr = ring && pb >= 0 && rend != ring_after(pb + a.msg);
-            a.rec[(long)c * a.max_rec + nrec] = lagr ? (pb | WALK_REC_LAG) : pb;
+            long* rp = a.rec + (long)c * a.max_rec + nrec;
+            if (lb) {  // published for the walkers that look back on this chunk
+                __hip_atomic_store(rp, rv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(a.pub + c, nrec + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                *rp = rv;
+            }
         }
-        if (pb >= core0 && pb < end) {  // in this chunk's core: one contiguous run of records
+        if (pb >= core0 && pb < cend) {  // in this chunk's core: one contiguous run of records
             if (ncore == 0) first_in = nrec;
             ++ncore;
+        }
+        if (lb && pb >= cend && pb < a.core_hi) {  // uniform: a frame of a later chunk's core
+            if (nrec >= a.max_rec) {               // overflow: the host falls back to the halo walk
+                nrec = a.max_rec + 1;
+                break;
+            }
+            int* lbres = reinterpret_cast<int*>(scr + 8);
+            if (t == 0) *lbres = lookback_find(a, pb, rv);
+            __syncthreads();
+            const int j = *lbres;
+            if (j >= 0) {  // this walk joins chunk m's from this frame on: done
+                if (t == 0) {
+                    a.link[3 * c] = (int)((pb - a.core_lo) / a.chunk);
+                    a.link[3 * c + 1] = nrec;
+                    a.link[3 * c + 2] = j;
+                }
+                ++nrec;
+                break;
+            }
         }
         past = pb >= end;
         // a frame of the next core located from a state before this core's
@@ -2547,6 +2616,12 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
         if (a.ncore) {
             a.ncore[c] = ncore;
             a.first_in[c] = first_in;
+        }
+        if (lb) {
+            // the walk's end: a walker still looking back on this chunk stops waiting
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(a.pub + c, min(nrec, a.max_rec) | WALK_PUB_DONE, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     }  // chunks
@@ -2738,6 +2813,207 @@ hipError_t launch_compact(const CompactArgs& a, hipStream_t st)
     // blocks (one CU's LDS was the limit: 16 binary searches per thread there)
     const long nb = std::max(1L, std::min(64L, (a.cap + 2047) / 2048));
     hipLaunchKernelGGL(compact_kernel, dim3((unsigned)nb), dim3(1024), 0, st, a);
+    return hipGetLastError();
+}
+
+// Look-back resolution (ResolveArgs). Every workgroup resolves the chain in
+// LDS (a few KB of links), then writes its share of the owned frames.
+//  - next[c] = the chunk c's walk joined (nchunks: none). Chunk 0's walk is
+//    true; a chain chunk's walk is true from its entry frame, so the chain
+//    0 -> next -> next ... is the sequential walk.
+//  - c is certainly on the chain when no chunk before it jumps past it
+//    (prefix max of next <= c: the increasing chain cannot step over c). These
+//    anchors are found by one scan; from each anchor one thread follows next
+//    to the following anchor, marking the chain chunks between (usually none)
+//    and setting each one's entry index from its predecessor's link.
+//  - each chain chunk contributes records [entry, shared frame) (the last: to
+//    its walk's end), trimmed to [own_lo, own_hi): only chunk 0 holds walk-in
+//    records and only the last chain chunk records past own_hi.
+__global__ void __launch_bounds__(1024) resolve_kernel(ResolveArgs a)
+{
+    constexpr int NT = 1024, NC = RESOLVE_MAX_CHUNKS, CPT = NC / NT, G = 2;
+    __shared__ int nxt[NC];
+    __shared__ int ent[NC];   // entry index; after the trim, the first owned record
+    __shared__ int excl[NC];  // exclusive scan of the owned counts
+    __shared__ unsigned char anc[NC], onc[NC];
+    __shared__ long wsum[NT / 64];
+    __shared__ int wmax[NT / 64];
+    __shared__ int sflags;
+    __shared__ long sexit[2];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int C = (int)a.nchunks, MR = a.max_rec;
+    if (t == 0) {
+        sflags = 0;
+        sexit[0] = -1;
+        sexit[1] = 0;
+    }
+    // 1. links (thread t: chunks t*CPT .. t*CPT + CPT-1), anchors by a prefix max
+    int nx[CPT];
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+        const int c = t * CPT + u, cc = min(c, C - 1);
+        const int m = a.link[3 * cc], nr = a.nrec[cc];
+        const bool ovf = nr > MR;
+        // an overflowed walk joins nothing; as c + 1 it does not hide later anchors
+        nx[u] = c >= C ? 0 : ovf ? c + 1 : (m >= 0 ? m : C);
+        if (c < C) {
+            nxt[c] = nx[u];
+            onc[c] = 0;
+        }
+    }
+    int tm = nx[0];
+#pragma unroll
+    for (int u = 1; u < CPT; ++u) tm = max(tm, nx[u]);
+    int inc = tm;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(inc, o);
+        if (lane >= o) inc = max(inc, y);
+    }
+    if (lane == 63) wmax[w] = inc;
+    __syncthreads();
+    int pm = __shfl_up(inc, 1);
+    if (lane == 0) pm = 0;
+    for (int u = 0; u < w; ++u) pm = max(pm, wmax[u]);
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+        const int c = t * CPT + u;
+        if (c < C) {
+            const bool an = c == 0 || pm <= c;
+            anc[c] = an;
+            if (an) onc[c] = 1;
+            pm = max(pm, nx[u]);
+        }
+    }
+    if (t == 0) ent[0] = 0;
+    __syncthreads();
+    // 2. the chain from each anchor to the next
+    for (int u = 0; u < CPT; ++u) {
+        const int c = t * CPT + u;
+        if (c < C && anc[c]) {
+            for (int x = c;;) {
+                const int y = nxt[x];
+                if (y >= C) break;
+                ent[y] = a.link[3 * x + 2];
+                onc[y] = 1;
+                if (anc[y]) break;
+                x = y;
+            }
+        }
+    }
+    __syncthreads();
+    // 3. each chain chunk's records, trimmed to the owned range
+    auto rpb = [](long r) { return r < 0 ? r : (r & WALK_REC_PB); };
+    int cnt[CPT], fi[CPT], cb[CPT], ce[CPT];
+    long own = 0, chn = 0;
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+        const int c = t * CPT + u;
+        cnt[u] = fi[u] = cb[u] = ce[u] = 0;
+        if (c < C && onc[c]) {
+            const int m = a.link[3 * c], nr = a.nrec[c];
+            const bool ovf = nr > MR;
+            int e = (m >= 0 && !ovf) ? a.link[3 * c + 1] : min(nr, MR), b = min(ent[c], e);
+            if (ovf) atomicOr(&sflags, RESOLVE_OVERFLOW);
+            cb[u] = b;
+            ce[u] = e;
+            const long* rc = a.rec + (long)c * MR;
+            if (c == 0 || m < 0 || ovf) {
+                for (int k = b; k < e; ++k)
+                    if (rpb(rc[k]) < 0) atomicOr(&sflags, RESOLVE_NEG_FRAME);
+                while (b < e && rpb(rc[b]) < a.own_lo) ++b;
+                while (e > b && rpb(rc[e - 1]) >= a.own_hi) --e;
+            }
+            if (m < 0 && !ovf) {  // the chain's last chunk: its exit state is the walk's
+                sexit[0] = a.exit_pos[c];
+                sexit[1] = a.exit_ring ? a.exit_ring[c] : 0;
+            }
+            cnt[u] = e - b;
+            fi[u] = b;
+        }
+        own += cnt[u];
+        chn += ce[u] - cb[u];
+    }
+    // block scan of (chain records << 32 | owned) in chunk order
+    long v = (chn << 32) | own, vi = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const long y = __shfl_up(vi, o);
+        if (lane >= o) vi += y;
+    }
+    if (lane == 63) wsum[w] = vi;
+    __syncthreads();
+    long off = vi - v, tot = 0;
+    for (int u = 0; u < NT / 64; ++u) {
+        if (u < w) off += wsum[u];
+        tot += wsum[u];
+    }
+    const long tot_own = tot & 0xffffffffL, tot_chn = tot >> 32;
+    long oo = off & 0xffffffffL, oc = off >> 32;
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+        const int c = t * CPT + u;
+        if (c < C) {
+            excl[c] = (int)oo;
+            ent[c] = fi[u];
+        }
+        oo += cnt[u];
+        if (blockIdx.x == 0 && a.chain) {  // every record of the true walk (shard reports)
+            const long* rc = a.rec + (long)c * MR;
+            for (int k = cb[u]; k < ce[u]; ++k, ++oc)
+                if (oc < a.chain_cap) a.chain[oc] = rc[k];
+        }
+    }
+    __syncthreads();
+    // 4. owned slots, spread over the workgroups: slot -> its chunk by binary
+    // search over the scan (last chunk with excl <= slot), then the record
+    const long lim = min(tot_own, a.cap);
+    for (long i0 = (long)blockIdx.x * NT * G; i0 < lim; i0 += (long)gridDim.x * NT * G) {
+        long pbv[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const long idx0 = i0 + g * NT + t;
+            const int idx = (int)(idx0 < lim ? idx0 : lim - 1);
+            int lo = 0, hi = C;
+#pragma unroll
+            for (int it = 0; it < 14; ++it) {  // C <= 8192 = 2^13
+                const int mid = (lo + hi) >> 1;
+                const bool go = hi - lo > 1;
+                const bool le = excl[mid] <= idx;
+                lo = go && le ? mid : lo;
+                hi = go && !le ? mid : hi;
+            }
+            pbv[g] = rpb(a.rec[(long)lo * MR + ent[lo] + (idx - excl[lo])]);
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const long idx = i0 + g * NT + t;
+            if (idx < lim) {
+                a.list[idx] = pbv[g];
+                if (a.list2) a.list2[idx] = pbv[g];
+            }
+        }
+    }
+    if (blockIdx.x == 0) {
+        // the walkers' publication counts and chunk counter, zero for the next call
+        for (int c = t; c < C; c += NT) a.pub[c] = 0;
+        if (t == 0) {
+            *a.count = tot_own;
+            if (a.queue_reset) *a.queue_reset = 0;
+            a.status[0] = tot_own;
+            a.status[1] = sflags;
+            a.status[2] = sexit[0];
+            a.status[3] = sexit[1];
+            a.status[4] = tot_chn;
+        }
+    }
+}
+
+hipError_t launch_resolve(const ResolveArgs& a, hipStream_t st)
+{
+    if (a.nchunks < 1 || a.nchunks > RESOLVE_MAX_CHUNKS) return hipErrorInvalidValue;
+    const long nb = std::max(1L, std::min(64L, (a.cap + 2047) / 2048));
+    hipLaunchKernelGGL(resolve_kernel, dim3((unsigned)nb), dim3(1024), 0, st, a);
     return hipGetLastError();
 }
 

@@ -137,7 +137,23 @@ struct WalkArgs {
     const double2* tw_m;        // WALK_FFT_M forward twiddles
     const double2* tspec;       // sum_j c_j e^{+2 pi i k j / M}, k < M
     double tspec_max;           // max_k |tspec_k| (error bound)
+    // Look-back stitching on the device (lookback = 1; needs `queue`): chunk
+    // c > 0 walks from its core start (minus halo) with no walk-in; past its
+    // core end it checks each frame it locates against the records the
+    // chunk owning that frame has published so far, and stops at the first
+    // frame they share (the two walks are one from there on). A walk that
+    // shares none walks on, through later cores, to core_hi. Records are
+    // published write-through (sc1) with a per-chunk count (pub, zero before
+    // the launch; | WALK_PUB_DONE when the chunk's walk ends); link[3c..3c+2]
+    // = {chunk m whose walk it joined (-1: none), index of the shared frame
+    // in c's records, its index in m's records}.
+    int lookback;
+    int* pub;
+    int* link;
 };
+constexpr int WALK_PUB_DONE = 1 << 30;
+// a walker waits at most this many polls for the chunk it looks back on
+constexpr int WALK_SPIN_MAX = 1 << 16;
 // A walk record is a preamble start, plus in ring mode the walk state after
 // the frame: (pb + message_len, ring end), where the ring end is the first
 // ring end past pb + message_len, or the one after it (the next buffer was
@@ -200,6 +216,35 @@ struct CompactArgs {
     int* queue_reset;           // nullable: the walkers' chunk counter, zeroed at the end
 };
 hipError_t launch_compact(const CompactArgs& a, hipStream_t st);
+
+// The look-back walk's true walk (WalkArgs::lookback), resolved on the device
+// in one workgroup: chunk 0 starts at the true state, so the chain 0 -> link
+// -> link ... of the chunks whose walks it joins is the sequential walk; each
+// chain chunk contributes its records from its entry index to the shared
+// frame. Outputs: the owned frames (pb in [own_lo, own_hi)) in walk order, the
+// whole chain's records (nullable), and a status block.
+constexpr int RESOLVE_MAX_CHUNKS = 8192;
+enum { RESOLVE_OVERFLOW = 1, RESOLVE_NEG_FRAME = 2 };
+struct ResolveArgs {
+    const long* rec;            // [chunk][max_rec]
+    const int* nrec;            // [chunk]
+    const int* link;            // [chunk][3]
+    const long* exit_pos;       // [chunk]
+    const long* exit_ring;      // [chunk] (nullable: ring off)
+    long nchunks;
+    int max_rec;
+    long own_lo, own_hi;        // owned preamble starts; own_lo = LONG_MIN: no lower bound
+    long cap;                   // list capacity
+    long* list;                 // owned preamble starts
+    long* list2;                // nullable: a second copy (the caller's pb_out)
+    long* count;                // owned frames (uncapped)
+    long* chain;                // nullable: every record of the true walk
+    long chain_cap;
+    long* status;               // {owned, flags (RESOLVE_*), exit pos, exit ring end, chain records}
+    int* pub;                   // zeroed for the next call
+    int* queue_reset;           // nullable: the walkers' chunk counter, zeroed
+};
+hipError_t launch_resolve(const ResolveArgs& a, hipStream_t st);
 
 hipError_t launch_stream_params(int logn, const StreamParamsArgs& a, hipStream_t st);
 // pilot_freq_sinh + the params stage fused (N = 512, 640-point CFO form);

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define OFDM_MI355X_ABI_VERSION 3
+#define OFDM_MI355X_ABI_VERSION 4
 
 enum {
     OFDM_OK = 0,
@@ -352,12 +352,13 @@ int ofdm_sync_frames(ofdm_ctx* ctx, double* frames, size_t nframes, size_t frame
  * samples past n read as zero (the walk ends once its scan passes n).
  * A frame the walk locates past the stream end stops the walk. A frame whose
  * preamble would start before sample 0 fails with OFDM_ERR_UNSUPPORTED.
- * The walk runs as parallel chunk walkers stitched into the one sequential
- * walk (chunk = samples per walker, 0 = automatic). Outputs (device, nullable):
+ * The walk runs as parallel chunk walkers joined into the one sequential
+ * walk on the device (chunk = samples per walker, 0 = automatic; see
+ * ofdm_walk_tuning). Outputs (device, nullable):
  * pb_out[f] preamble start, bytes_out (bytes_per_frame per frame),
  * constell_out (D*num_symb complex per frame), cfo_out. *nframes_out = frames
  * found; outputs hold the first max_frames. The input is not modified.
- * Returns once the host has stitched the walk (it waits for the walk records);
+ * Returns once the walk is resolved (the host waits for a small status block);
  * the decode is enqueued on `stream` and may still be running, so order later
  * work on `stream`, or synchronise it, before reading the outputs. */
 int ofdm_rx_stream(ofdm_ctx* ctx, const double* iq, size_t n, size_t max_frames, long chunk,
@@ -370,7 +371,7 @@ int ofdm_rx_stream_i16(ofdm_ctx* ctx, const int16_t* iq16, size_t n, size_t max_
                        long* pb_out, uint8_t* bytes_out, double* constell_out, double* cfo_out,
                        size_t* nframes_out, void* stream);
 
-/* rx.cpp's SDR ring for the stream walk: R samples per refill (>= 2 *
+/* rx.cpp's SDR ring for the stream walk: R samples per refill (>=
  * output_size), 0 = the continuous walk. Default: rx_buf_size * output_size. */
 int ofdm_set_stream_ring(ofdm_ctx* ctx, long ring);
 int ofdm_get_stream_ring(const ofdm_ctx* ctx, long* ring);
@@ -425,9 +426,16 @@ int ofdm_stream_shard_margins(const ofdm_ctx* ctx, long* halo_out, long* tail_ou
 /* ---- stream walk tuning (tests and experiments) --------------------------
  * Per-context settings of the ofdm_rx_stream* walkers; ofdm_create sets the
  * defaults (ofdm_walk_tuning_default), which are the product configuration.
- * chunks_per_slot, halo_milli and ext_milli change only how the walk is
- * split over walkers: the stitched walk is exact for any values (short halos
- * cost serial re-walks). exact_search = 1 replaces the certified FFT
+ * chunks_per_slot, halo_milli, ext_milli and lookback change only how the
+ * walk is split over walkers: the stitched walk is exact for any values.
+ * lookback = 1 (default): each chunk's walker starts at its core (minus
+ * halo_milli, default 0) and walks on past the core end until its walk
+ * shares a frame with the records the next chunk's walker has published;
+ * the chain of joined walks, resolved on the device, is the sequential walk
+ * (no host stitching, no re-walks). lookback = 0: every chunk walks in from a
+ * halo (default 3 frames) and the host stitches the walks, re-walking a chunk
+ * whose walk-in missed the true walk (short halos cost serial re-walks).
+ * halo_milli = -1 selects the mode's default. exact_search = 1 replaces the certified FFT
  * preamble search by the reference's serial recurrence; t2_f32 = 0 turns the
  * FP32 T2 screen off (FP64 only). t2_margin is the FP32 screen's
  * certification margin: at or above the default 4e-5 every uncertain block is
@@ -439,7 +447,8 @@ int ofdm_stream_shard_margins(const ofdm_ctx* ctx, long* halo_out, long* tail_ou
  * kernel (same results within the parity bar; for A/B measurements). */
 typedef struct ofdm_walk_tuning {
     long chunks_per_slot; /* chunks per resident walker (>= 1; default 1)       */
-    long halo_milli;      /* walk-in halo, 1/1000 frames (default 3000)         */
+    long halo_milli;      /* walk-in halo, 1/1000 frames (-1 = default: 0 with
+                             lookback, 3000 without)                            */
     long ext_milli;       /* walk-on past the core end, 1/1000 frames (0)       */
     int exact_search;     /* 1: serial-recurrence preamble search (default 0)   */
     int t2_f32;           /* 1: certified FP32 T2 screen (default 1)            */
@@ -448,6 +457,7 @@ typedef struct ofdm_walk_tuning {
     int staged_decode;    /* 1: decode located frames with the staged cfo ->
                              params -> rx kernels even where a fused decode
                              kernel fits (A/B measurements, tests; default 0) */
+    int lookback;         /* 1: device-side look-back stitching (default 1)     */
 } ofdm_walk_tuning;
 int ofdm_walk_tuning_default(ofdm_walk_tuning* out);
 int ofdm_get_walk_tuning(const ofdm_ctx* ctx, ofdm_walk_tuning* out);

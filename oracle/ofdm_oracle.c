@@ -622,8 +622,18 @@ static cplx sample_or_zero(const cplx* x, long n, long i) { return (i >= 0 && i 
 /* PREAMBLE_FORM::find_preamble, Frame.cpp:338-378 (first threshold crossing,
  * running energy updated after each test). Samples past n read as 0 (the
  * reference reads past its vector there). Returns start+lag or -10. */
+static long find_preamble_lag(const ofdm_params* p, const double* templd, const double* xd, long n, long start);
+
 long orc_find_preamble(const ofdm_params* p, const double* templd, const double* xd, long n,
                        long start)
+{
+    const long lag = find_preamble_lag(p, templd, xd, n, start);
+    return lag < 0 ? -10 : start + lag;
+}
+
+/* The same search, returning the passing lag (>= 0) or -1: in stream
+ * coordinates start + lag may be any value, -10 included. */
+static long find_preamble_lag(const ofdm_params* p, const double* templd, const double* xd, long n, long start)
 {
     const cplx* c = (const cplx*)templd;
     const cplx* x = (const cplx*)xd;
@@ -640,13 +650,13 @@ long orc_find_preamble(const ofdm_params* p, const double* templd, const double*
         if (norm > 1.0) {
             cplx energy = 0;
             for (int j = 0; j < L; j++) energy += sample_or_zero(x, n, base + j) * c[j];
-            if (cabs(energy) / sqrt(norm) > level) return i + start;
+            if (cabs(energy) / sqrt(norm) > level) return i;
         }
         cplx a = sample_or_zero(x, n, base + L), b = sample_or_zero(x, n, base);
         norm += creal(a) * creal(a) + cimag(a) * cimag(a);
         norm -= creal(b) * creal(b) + cimag(b) * cimag(b);
     }
-    return -10;
+    return -1;
 }
 
 /* PREAMBLE_FORM::chan_char_lq, Frame.hpp:389-434: FFT of the preamble form
@@ -903,7 +913,8 @@ static double t2_block_rel_at(int size, const double* mask, const cplx* x, long 
  *     restarted at output_size (:137-145);
  *   hit >= ring_end - output_size -> ring_end += R: the carry at
  *     pos >= threshold (:147-156);
- *   pb = find_preamble(hit) + 1; pb < -2 -> pos = hit + message.size (:160-166);
+ *   pb = find_preamble(hit) + 1; no preamble (-10) -> pos = hit + message.size
+ *     (:160-166; a found preamble may have pb < 0 here, in the zero header);
  *   pb >= ring_end - output_size + T2sin_size -> ring_end += R (:180-189);
  *   record pb; pos = pb + message.size (:198).
  * Every sample a step reads lies in the buffer, so the decoded frames are the
@@ -985,11 +996,15 @@ long orc_stream_walk_ring(const ofdm_params* p, const double* xd, long n, long r
             continue;
         }
         if (ring && hit >= rend - out) rend += ring;
-        const long pb = orc_find_preamble(p, (const double*)templ, xd, n, hit) + 1;
-        if (pb < -2) {
+        /* rx.cpp:160-168 tests preamble_begin < -2 in buffer coordinates,
+         * where a found preamble gives >= 1; here a found preamble may lie in
+         * the ring's zero header (pb < 0), so the test is on the search */
+        const long lag = find_preamble_lag(p, (const double*)templ, xd, n, hit);
+        if (lag < 0) {
             pos = hit + msg;
             continue;
         }
+        const long pb = hit + lag + 1;
         if (ring && pb >= rend - out + size) rend += ring;
         if (pb + pre + msg > n) break;
         if (nf < max) {

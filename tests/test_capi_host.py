@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in declared if not hasattr(L, n)]
     assert missing == []
     assert set(declared) == set(M.SIGNATURES), "python binding out of sync with the header"
-    assert L.ofdm_abi_version() == 3
+    assert L.ofdm_abi_version() == 4
 
 
 def test_params_default_is_committed_config():

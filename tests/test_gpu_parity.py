@@ -472,3 +472,63 @@ def test_full_size_config_b_every_frame_matches_oracle():
     ocons, obytes, _ = O.rx_batch(B, h, nf, g["message_len"], threads=16)
     assert np.array_equal(host(out), obytes)
     assert rel_err(host(cons), ocons) < 1e-9
+
+
+def _bit_errors(a: np.ndarray, b: np.ndarray) -> int:
+    return int(np.unpackbits(np.bitwise_xor(a, b)).sum())
+
+
+def test_config3_bench_workload_every_frame_matches_oracle():
+    """bench.py's config-3 record at its size (BASELINE
+    configs[2]): the 4 096 config-C frames per GPU (N = 4096, D = 2048, P = 64,
+    cp = 1024, 16-QAM) of the job's counter-based payload, tx with fused AWGN at
+    Es/N0 = 10 dB (seed 1010), then rx: every frame's bytes equal the oracle's
+    rx of the same noisy samples, the constellation to 1e-9 (OFDM/modulation.cpp:
+    53-87, Frame.cpp:73-96). Two BER-sweep points (4 and 16 dB, seed 1000 + SNR,
+    the sweep's frame count): the GPU's bit-error counts equal the oracle's
+    decisions on the same IQ, bit for bit.
+    The channel is this repo's counter-based AWGN, not modem arithmetic: the
+    GPU draws its Box-Muller on the FP32 transcendental units, so its noise
+    agrees with the oracle's FP64 draw of the same counters to the channel
+    model's tolerance, 1e-6 relative on the noise component (measured ~1e-7);
+    the modem's own 1e-6 IQ bound applies to the noise-free tx (1e-10 here)."""
+    from ofdm_synth import payload_bytes
+    m = modem("C")
+    g = O.geometry(CC)
+    nf, msg, bpf = 4096, g["message_len"], g["bytes_per_frame"]
+    es = 10.0 / 9.0  # mean energy of the reference's 16-QAM table (bench.py config3_leg)
+    data = payload_bytes(0, nf * bpf)
+    d = dev(data)
+    iq = torch.empty((nf * msg,), dtype=torch.complex128, device="cuda")
+    cons = torch.empty((nf * g["npts"],), dtype=torch.complex128, device="cuda")
+    out = torch.empty_like(d)
+    errs = torch.zeros((1,), dtype=torch.int64, device="cuda")
+    std = float(np.sqrt(es / 10 ** (10.0 / 10)))
+    m.tx(d, nf, iq, noise_std=std, seed=1010, sample_offset=0)
+    m.rx(iq, nf, constell_out=cons, bytes_out=out, ref=d, bit_errors=errs)
+    h = host(iq)
+    ocons, obytes, _ = O.rx_batch(CC, h, nf, msg, threads=16)
+    hb = host(out)
+    assert np.array_equal(hb, obytes)  # every frame, every byte
+    assert rel_err(host(cons), ocons) < 1e-9
+    assert int(host(errs)[0]) == _bit_errors(obytes, data)
+    del ocons, cons
+    # the channel: noise component against the oracle's draw of the same counters
+    f_chk = [0, 1, 2047, 4095]
+    for f in f_chk:
+        clean = O.tx_batch(CC, data[f * bpf:(f + 1) * bpf], 1)
+        want = O.awgn(clean, std, seed=1010, sample_offset=f * msg)
+        got = h[f * msg:(f + 1) * msg]
+        assert rel_err(got - clean, want - clean) < 1e-6
+    del h
+    # two BER-sweep points: GPU bit-error counts == the oracle's on the same IQ
+    nb = int(np.ceil(1e7 / (8 * bpf)))
+    for db in (4, 16):
+        errs.zero_()
+        sd = float(np.sqrt(es / 10 ** (db / 10)))
+        m.tx(d, nb, iq, noise_std=sd, seed=1000 + db, sample_offset=0)
+        m.rx(iq, nb, bytes_out=out, ref=d, bit_errors=errs)
+        hn = host(iq)[:nb * msg]
+        _, ob, _ = O.rx_batch(CC, hn, nb, msg, threads=16)
+        assert np.array_equal(host(out)[:nb * bpf], ob)
+        assert int(host(errs)[0]) == _bit_errors(ob, data[:nb * bpf]) > 0

@@ -114,12 +114,13 @@ def test_stream_continuous_walk_matches_oracle():
         assert np.array_equal(want, O.stream_walk(D, x))
 
 
-# rx.cpp's ring with 2- and 3-frame refills: a ring end every ~2 frames of the
-# stream, so most steps meet a refill (misses that restart the grid, carries)
-RING_CFGS = [dict(D, rx_buf_size=2), dict(D, rx_buf_size=3)]
+# rx.cpp's ring with 1-, 2- and 3-frame refills: a ring end every ~1-2 frames
+# of the stream, so most steps meet a refill (misses that restart the grid,
+# carries; rx_buf_size = 1, R = output_size, is the smallest ring a config makes)
+RING_CFGS = [dict(D, rx_buf_size=2), dict(D, rx_buf_size=3), dict(D, rx_buf_size=1)]
 
 
-@pytest.mark.parametrize("rcfg", RING_CFGS, ids=["rb2", "rb3"])
+@pytest.mark.parametrize("rcfg", RING_CFGS, ids=["rb2", "rb3", "rb1"])
 @pytest.mark.parametrize("chunk", [0, 5000, 9000, 20000])
 def test_stream_ring_walk_matches_rx_cpp_loop(rcfg, chunk):
     x, data = impaired_stream(rcfg, 40, seed=4)
@@ -148,13 +149,16 @@ def test_stream_wire_capture_with_exact_zero_gaps(ring, chunk):
     assert got[0] == len(want) and np.array_equal(got[1], want)
 
 
+@pytest.mark.parametrize("lookback", [0, 1], ids=["host_stitch", "lookback"])
 @pytest.mark.parametrize("halo,ext", [(0, 0), (250, 0), (100, 2000)])
 @pytest.mark.parametrize("chunk", [5000, 20000])
-def test_stream_ring_short_halo_rewalks(halo, ext, chunk):
-    # re-walks from ring states (position and ring end) stay exact
+def test_stream_ring_short_halo_rewalks(halo, ext, chunk, lookback):
+    # host stitching: re-walks from ring states (position and ring end) stay
+    # exact; look-back: walks joined on ring states (the record's lag bit)
     rcfg = RING_CFGS[1]
     x, data = impaired_stream(rcfg, 40, seed=6, gap_max=6000)
-    check_against_oracle(rcfg, x, run_stream(rcfg, x, chunk=chunk, tuning=dict(halo_milli=halo, ext_milli=ext)))
+    check_against_oracle(rcfg, x, run_stream(rcfg, x, chunk=chunk,
+                                             tuning=dict(halo_milli=halo, ext_milli=ext, lookback=lookback)))
 
 
 def test_stream_ring_validation_and_state():
@@ -162,22 +166,42 @@ def test_stream_ring_validation_and_state():
     g = O.geometry(D)
     assert m.stream_ring() == 40 * g["frame_len"] == O.ring_len(D)  # rx_buf_size * output_size
     assert m.initial_state() == (-g["frame_len"], 40 * g["frame_len"])
-    for bad in (-1, g["frame_len"]):
+    for bad in (-1, g["frame_len"] - 1):
         with pytest.raises(M.OfdmError):
             m.stream_ring(bad)
+    old = m.stream_ring(g["frame_len"])  # R = output_size (rx_buf_size = 1) is accepted
+    m.stream_ring(old)
     old = m.stream_ring(0)
     assert m.initial_state() == (0, 0)
     m.stream_ring(old)
 
 
+@pytest.mark.parametrize("lookback", [0, 1], ids=["host_stitch", "lookback"])
 @pytest.mark.parametrize("halo,ext", [(0, 0), (100, 0), (250, 0), (500, 0), (100, 2000), (1500, 2000)])
 @pytest.mark.parametrize("chunk", [0, 9000, 20000])
-def test_stream_short_halo_rewalks_match_sequential_walk(halo, ext, chunk):
-    # walk-in halos (in 1/1000 frames) too short to meet the true walk force
-    # re-walks from the previous chunk's hand-over state (with or without the
-    # walk-on past the core end): still exact
+def test_stream_short_halo_rewalks_match_sequential_walk(halo, ext, chunk, lookback):
+    # host stitching: walk-in halos (in 1/1000 frames) too short to meet the
+    # true walk force re-walks from the previous chunk's hand-over state (with
+    # or without the walk-on past the core end); look-back: any halo, the
+    # walks join on the device. Still exact
     x, data = impaired_stream(D, 40, seed=4)
-    check_against_oracle(D, x, run_stream(D, x, chunk=chunk, tuning=dict(halo_milli=halo, ext_milli=ext)))
+    check_against_oracle(D, x, run_stream(D, x, chunk=chunk,
+                                          tuning=dict(halo_milli=halo, ext_milli=ext, lookback=lookback)))
+
+
+@pytest.mark.parametrize("ring", [None, 0], ids=["ring", "continuous"])
+@pytest.mark.parametrize("nf,chunk,halo", [(40, 1500, 0), (40, 2500, 0), (40, 6000, 0), (40, 13000, 0),
+                                           (120, 300, 100)])
+def test_stream_lookback_chain_across_chunks(nf, chunk, halo, ring):
+    # look-back with chunks shorter than a frame (5 760 samples): most cores
+    # hold no frame start, a walk joins a chunk several cores ahead, and the
+    # chain resolution passes over chunks no walk joins (non-anchor chunks).
+    # 120 frames in 300-sample chunks: more chunks than resident walkers, so
+    # walkers wait on chunks taken from the queue after theirs. Every frame
+    # against the oracle's walk
+    x, data = impaired_stream(D, nf, seed=7, gap_max=6000)
+    got = run_stream(D, x, chunk=chunk, ring=ring, tuning=dict(halo_milli=halo))
+    check_against_oracle(D, x, got, ring=ring)
 
 
 def test_stream_walk_certified_search_equals_serial_recurrence():
@@ -407,8 +431,12 @@ def test_walk_tuning_defaults_and_validation():
     m = modem(D)
     t = M.WalkTuning()
     M.check(M.lib().ofdm_get_walk_tuning(m.h, C.byref(t)))
-    assert (t.chunks_per_slot, t.halo_milli, t.ext_milli, t.exact_search, t.t2_f32) == (1, 3000, 0, 0, 1)
-    assert t.t2_margin == 4e-5
+    assert (t.chunks_per_slot, t.halo_milli, t.ext_milli, t.exact_search, t.t2_f32) == (1, -1, 0, 0, 1)
+    assert t.t2_margin == 4e-5 and t.lookback == 1
+    with pytest.raises(M.OfdmError):
+        m.walk_tuning(lookback=2)
+    with pytest.raises(M.OfdmError):
+        m.walk_tuning(halo_milli=-2)
     with pytest.raises(M.OfdmError):
         m.walk_tuning(chunks_per_slot=0)
     with pytest.raises(M.OfdmError):

@@ -92,7 +92,7 @@ def test_ring_walk_is_rx_cpp_loop():
     differs = 0
     for seed, nf, gap in [(4, 24, 4096), (5, 60, 3000), (7, 40, 0), (8, 40, 12000)]:
         x, _ = impaired_stream(D, nf, seed=seed, gap_max=gap)
-        for rb in (2, 3, 5, 40):
+        for rb in (1, 2, 3, 5, 40):
             cfg = dict(D, rx_buf_size=rb)
             a = O.stream_walk_ring(cfg, x)[0]
             b = O.rx_app_walk(cfg, x)
