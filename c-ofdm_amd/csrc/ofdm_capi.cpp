@@ -1409,7 +1409,10 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     chunk = std::max(chunk, (long)c->t2);
     const long nchunks = std::max(1L, (span_w + chunk - 1) / chunk);
     if (nchunks > 1 << 20) return fail(OFDM_ERR_INVALID, "chunk too small for this stream");
-    const bool lbk = tu.lookback && !force_halo && nchunks <= ofdm::RESOLVE_MAX_CHUNKS;
+    // look-back needs a resolvable chunk count and per-chunk record counts
+    // below 2^14 (the resolve kernel's packing): else the halo walk
+    bool lbk = tu.lookback && !force_halo && nchunks <= ofdm::RESOLVE_MAX_CHUNKS &&
+               (2 * chunk + std::max(0L, own_lo - start)) / msg < 8192;
     const long halo = (tu.halo_milli < 0 ? (lbk ? 0L : 3000L) : tu.halo_milli) * flen / 1000;
     const long ext = std::max(0L, tu.ext_milli) * flen / 1000;
     // each located frame advances the walk by > message_len, and a walker can
@@ -1520,8 +1523,33 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
         w.pub = static_cast<int*>(c->s_pub.p);
         w.link = d_link;
     }
+    // diagnostics: OFDM_WALK_PROF=<file> appends one JSON line per call with
+    // every chunk's walker timeline (WalkArgs::prof)
+    const char* prof_path = getenv("OFDM_WALK_PROF");
+    long* d_prof = nullptr;
+    if (prof_path) HIP_TRY(hipMalloc((void**)&d_prof, (size_t)nchunks * ofdm::WALK_PROF_FIELDS * sizeof(long)));
+    w.prof = d_prof;
     hipError_t e = ofdm::launch_stream_walk(c->t2_logn, w, std::min(nchunks, slots), st);
     if (e != hipSuccess) return hip_fail(e, "stream_walk launch");
+    if (d_prof) {
+        std::vector<long> hp((size_t)nchunks * ofdm::WALK_PROF_FIELDS);
+        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(hipMemcpy(hp.data(), d_prof, hp.size() * sizeof(long), hipMemcpyDeviceToHost));
+        HIP_TRY(hipFree(d_prof));
+        if (FILE* f = fopen(prof_path, "a")) {
+            fprintf(f, "{\"nchunks\": %ld, \"chunk\": %ld, \"lookback\": %d, \"grid\": %ld, \"fields\": "
+                       "[\"t0\", \"t_core\", \"t_end\", \"ext_frames\", \"waits\", \"block\", \"xcc\", \"nrec\"], "
+                       "\"chunks\": [", nchunks, chunk, (int)lbk, std::min(nchunks, slots));
+            for (long k = 0; k < nchunks; ++k) {
+                fprintf(f, "%s[", k ? "," : "");
+                for (int i = 0; i < ofdm::WALK_PROF_FIELDS; ++i)
+                    fprintf(f, "%s%ld", i ? "," : "", hp[(size_t)k * ofdm::WALK_PROF_FIELDS + i]);
+                fprintf(f, "]");
+            }
+            fprintf(f, "]}\n");
+            fclose(f);
+        }
+    }
 
     // Fused decode: three kernels read each frame from the stream in place
     // (pilot_freq_sinh; the other sync stages' parameters + chan_char_lq;

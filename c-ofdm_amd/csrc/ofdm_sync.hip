@@ -2153,11 +2153,12 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
 // index of r in m's published records, or -1 when m's walk does not hold it
 // (m published a record past pb, or finished). While m has not reached pb
 // the walker waits for it, but only once m has been taken from the queue: its
-// walker is then resident, and it publishes every record before any wait of
-// its own, so the wait ends. Records and counts are stored write-through
+// walker is then resident (the grid is at most the resident walker count),
+// and it publishes every record before any wait of its own, so the wait
+// ends. Records and counts are stored write-through
 // (sc1) by the publishing lane, which drains its stores before each count;
 // every load here is an sc1 load of them.
-__device__ int lookback_find(const WalkArgs& a, long pb, long r)
+__device__ int lookback_find(const WalkArgs& a, long pb, long r, long* prof)
 {
     const long m = (pb - a.core_lo) / a.chunk;
     const long* rm = a.rec + m * a.max_rec;
@@ -2171,8 +2172,12 @@ __device__ int lookback_find(const WalkArgs& a, long pb, long r)
             if ((v < 0 ? v : (v & WALK_REC_PB)) > pb) return -1;  // m's walk passed pb without this frame
         }
         if (pv & WALK_PUB_DONE) return -1;
-        if (spin >= WALK_SPIN_MAX || __hip_atomic_load(a.queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= m)
+        // taken: a first-round chunk (m < grid: every workgroup of the grid
+        // is resident), or one the queue has handed out
+        if (spin >= WALK_SPIN_MAX ||
+            (m >= gridDim.x && __hip_atomic_load(a.queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + (long)gridDim.x <= m))
             return -1;  // m not taken yet: walk on (always exact), and look again at the next frame
+        if (prof) ++prof[4];
         __builtin_amdgcn_s_sleep(4);
     }
 }
@@ -2199,7 +2204,7 @@ struct WalkLds {
     }
 };
 
-template <int LOGT, bool I16>
+template <int LOGT, bool I16, bool PROF = false>
 __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(WalkArgs a)
 {
     constexpr int N = 1 << LOGT, T = N / 8, WT = WalkShape<LOGT>::WT, G = WalkShape<LOGT>::G;
@@ -2249,15 +2254,23 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
         for (int i = 0; i < 6; ++i) bslot[i] = INT_MAX;
     }
     int sl = 0;  // the slot of the next T2 evaluation (uniform; cycles 0, 1, 2)
-    // chunks: from the queue until it is drained (walkers that run slower on
-    // their CU take fewer), or the workgroup's one chunk
+    // chunks: the workgroup's own (its blockIdx), then from the queue until
+    // it is drained (walkers that run slower on their CU take fewer); or the
+    // one chunk of a re-walk launch. The first chunk takes no atomic: one
+    // counter serves ~88 dequeues per us, and 2048 walkers taking their first
+    // chunk from it started over ~24 us
     for (int round = 0;; ++round) {
     int c;
     if (a.queue) {
-        if (t0 == 0) *qslot = atomicAdd(a.queue, 1);
-        __syncthreads();
-        c = *qslot;
-        __syncthreads();  // every thread has read the slot
+        if (round == 0) {
+            c = (int)blockIdx.x;
+        } else {
+            if ((long)gridDim.x >= a.nchunks) break;  // uniform: no chunk left for the queue
+            if (t0 == 0) *qslot = (int)gridDim.x + atomicAdd(a.queue, 1);
+            __syncthreads();
+            c = *qslot;
+            __syncthreads();  // every thread has read the slot
+        }
         if ((long)c >= a.nchunks) break;
     } else {
         if (round > 0) break;
@@ -2274,6 +2287,14 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
     // look-back link {chunk this walk joins, the shared frame's index here and
     // there}: none until the walk joins one
     if (lb && t0 == 0) a.link[3 * c] = -1;
+    // diagnostics (a.prof): stored as they happen, nothing held in registers
+#define WALK_PROF (PROF ? a.prof + (long)c * WALK_PROF_FIELDS : nullptr)
+    if (long* prof = WALK_PROF; prof && t0 == 0) {
+        prof[0] = (long)wall_clock64();
+        prof[1] = 0;
+        prof[3] = 0;
+        prof[4] = 0;
+    }
     long pos = a.start_pos ? a.start_pos[blockIdx.x] : (c == 0 ? a.start : (core0 > a.halo ? core0 - a.halo : 0));
     const bool ring = a.ring > 0;  // uniform
     // ring mode: the first ring end after position q (the ring ends lie on
@@ -2579,13 +2600,17 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
             if (ncore == 0) first_in = nrec;
             ++ncore;
         }
+        if (long* prof = WALK_PROF; prof && pb >= cend && t == 0) {
+            if (prof[3] == 0) prof[1] = (long)wall_clock64();
+            ++prof[3];
+        }
         if (lb && pb >= cend && pb < a.core_hi) {  // uniform: a frame of a later chunk's core
             if (nrec >= a.max_rec) {               // overflow: the host falls back to the halo walk
                 nrec = a.max_rec + 1;
                 break;
             }
             int* lbres = reinterpret_cast<int*>(scr + 8);
-            if (t == 0) *lbres = lookback_find(a, pb, rv);
+            if (t == 0) *lbres = lookback_find(a, pb, rv, WALK_PROF);
             __syncthreads();
             const int j = *lbres;
             if (j >= 0) {  // this walk joins chunk m's from this frame on: done
@@ -2610,6 +2635,14 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
         pos = pb + a.msg;  // rx.cpp:192
     }
     if (t0 == 0) {
+        if (long* prof = WALK_PROF) {
+            unsigned xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            prof[2] = (long)wall_clock64();
+            prof[5] = blockIdx.x;
+            prof[6] = xcc & 0xf;
+            prof[7] = nrec;
+        }
         a.nrec[c] = nrec;
         a.exit_pos[c] = exitp;
         if (a.exit_ring) a.exit_ring[c] = exitr;
@@ -2625,6 +2658,7 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
         }
     }
     }  // chunks
+#undef WALK_PROF
 }
 
 __global__ void gather_kernel(GatherArgs a)
@@ -2649,6 +2683,20 @@ static hipError_t walk_launch_n(const WalkArgs& a, long nblocks, hipStream_t st)
     const size_t shm = walk_shm<LOGT>(a.L, a.cycles, a.tspec != nullptr);
     if (shm > 160 * 1024) return hipErrorInvalidValue;
     if ((a.iq16 != nullptr) == (a.iq != nullptr)) return hipErrorInvalidValue;  // exactly one stream format
+    if constexpr (LOGT == 8) {  // the diagnostics build of the default T2 size (OFDM_WALK_PROF)
+        if (a.prof) {
+            const void* k = a.iq16 ? (const void*)stream_walk_kernel<LOGT, true, true>
+                                   : (const void*)stream_walk_kernel<LOGT, false, true>;
+            lds_opt_in(k, 160 * 1024);
+            if (a.iq16)
+                hipLaunchKernelGGL((stream_walk_kernel<LOGT, true, true>), dim3((unsigned)nblocks),
+                                   dim3(WalkShape<LOGT>::WT), shm, st, a);
+            else
+                hipLaunchKernelGGL((stream_walk_kernel<LOGT, false, true>), dim3((unsigned)nblocks),
+                                   dim3(WalkShape<LOGT>::WT), shm, st, a);
+            return hipGetLastError();
+        }
+    }
     if (a.iq16) {
         lds_opt_in((const void*)stream_walk_kernel<LOGT, true>, 160 * 1024);
         hipLaunchKernelGGL((stream_walk_kernel<LOGT, true>), dim3((unsigned)nblocks), dim3(WalkShape<LOGT>::WT), shm,
@@ -2831,39 +2879,77 @@ hipError_t launch_compact(const CompactArgs& a, hipStream_t st)
 //    records and only the last chain chunk records past own_hi.
 __global__ void __launch_bounds__(1024) resolve_kernel(ResolveArgs a)
 {
-    constexpr int NT = 1024, NC = RESOLVE_MAX_CHUNKS, CPT = NC / NT, G = 2;
-    __shared__ int nxt[NC];
+    constexpr int NT = 1024, NC = RESOLVE_MAX_CHUNKS, UP = NC / NT, G = 2, TR = 8;
+    __shared__ int nxt[NC];   // the chunk c's walk joins (C: none)
+    __shared__ int jx[NC];    // its entry index there; after the chain pass, the owned-count scan
+    __shared__ int sege[NC];  // segment end (the shared frame; back-trimmed) | back trim << 16 | SEG_OVF
+    constexpr int SEG_OVF = 1 << 30;
     __shared__ int ent[NC];   // entry index; after the trim, the first owned record
-    __shared__ int excl[NC];  // exclusive scan of the owned counts
     __shared__ unsigned char anc[NC], onc[NC];
     __shared__ long wsum[NT / 64];
     __shared__ int wmax[NT / 64];
-    __shared__ int sflags;
+    __shared__ int sflags, sfront;
     __shared__ long sexit[2];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int C = (int)a.nchunks, MR = a.max_rec;
+    auto rpb = [](long r) { return r < 0 ? r : (r & WALK_REC_PB); };
     if (t == 0) {
         sflags = 0;
+        sfront = 0;
         sexit[0] = -1;
         sexit[1] = 0;
     }
-    // 1. links (thread t: chunks t*CPT .. t*CPT + CPT-1), anchors by a prefix max
-    int nx[CPT];
+    // 1. every global read of the chain pass at once: links and counts
+    // (chunks t + NT*u, coalesced), then the few records the trims need
+    int lm[UP], li[UP], lj[UP], nr[UP];
 #pragma unroll
-    for (int u = 0; u < CPT; ++u) {
-        const int c = t * CPT + u, cc = min(c, C - 1);
-        const int m = a.link[3 * cc], nr = a.nrec[cc];
-        const bool ovf = nr > MR;
-        // an overflowed walk joins nothing; as c + 1 it does not hide later anchors
-        nx[u] = c >= C ? 0 : ovf ? c + 1 : (m >= 0 ? m : C);
-        if (c < C) {
-            nxt[c] = nx[u];
-            onc[c] = 0;
-        }
+    for (int u = 0; u < UP; ++u) {
+        const int c = min(t + NT * u, C - 1);
+        lm[u] = a.link[3 * c];
+        li[u] = a.link[3 * c + 1];
+        lj[u] = a.link[3 * c + 2];
+        nr[u] = a.nrec[c];
     }
-    int tm = nx[0];
+    __syncthreads();  // sflags / sfront initialised
 #pragma unroll
-    for (int u = 1; u < CPT; ++u) tm = max(tm, nx[u]);
+    for (int u = 0; u < UP; ++u) {
+        const int c = t + NT * u;
+        if (c >= C) continue;
+        const bool ovf = nr[u] > MR;
+        // an overflowed walk joins nothing; as c + 1 it hides no later anchor
+        nxt[c] = ovf ? c + 1 : (lm[u] >= 0 ? lm[u] : C);
+        jx[c] = lj[u];
+        onc[c] = 0;
+        int e = (lm[u] >= 0 && !ovf) ? li[u] : min(nr[u], MR), bt = 0;
+        const long* rc = a.rec + (long)c * MR;
+        if (c == 0) {  // walk-in records before own_lo (records rise along the walk)
+            long r[TR];
+#pragma unroll
+            for (int k = 0; k < TR; ++k) r[k] = rc[min(k, max(e - 1, 0))];
+            int f = 0;
+            if (e > 0 && rpb(r[0]) < 0) atomicOr(&sflags, RESOLVE_NEG_FRAME);
+#pragma unroll
+            for (int k = 0; k < TR; ++k) f += (k < e && rpb(r[k]) < a.own_lo) ? 1 : 0;
+            while (f >= TR && f < e && rpb(rc[f]) < a.own_lo) ++f;  // longer walk-ins (rare)
+            sfront = f;
+        }
+        if (lm[u] < 0 && !ovf) {  // a walk that ended: the chain's last chunk if on it; records past own_hi
+            long r[TR];
+#pragma unroll
+            for (int k = 0; k < TR; ++k) r[k] = rc[max(e - 1 - k, 0)];
+#pragma unroll
+            for (int k = 0; k < TR; ++k) bt += (bt == k && k < e && rpb(r[k]) >= a.own_hi) ? 1 : 0;
+            while (bt < e && bt >= TR && rpb(rc[e - 1 - bt]) >= a.own_hi) ++bt;
+        }
+        sege[c] = (e - bt) | (bt << 16) | (ovf ? SEG_OVF : 0);
+    }
+    __syncthreads();
+    // 2. anchors: chunk c is on the chain when no chunk before it jumps past
+    // it (exclusive prefix max of nxt <= c), contiguous chunks per thread
+    const int CPT = (C + NT - 1) / NT, c0 = t * CPT;
+    int tm = 0;
+    for (int u = 0; u < CPT; ++u)
+        if (c0 + u < C) tm = max(tm, nxt[c0 + u]);
     int inc = tm;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -2875,26 +2961,25 @@ __global__ void __launch_bounds__(1024) resolve_kernel(ResolveArgs a)
     int pm = __shfl_up(inc, 1);
     if (lane == 0) pm = 0;
     for (int u = 0; u < w; ++u) pm = max(pm, wmax[u]);
-#pragma unroll
     for (int u = 0; u < CPT; ++u) {
-        const int c = t * CPT + u;
+        const int c = c0 + u;
         if (c < C) {
             const bool an = c == 0 || pm <= c;
             anc[c] = an;
             if (an) onc[c] = 1;
-            pm = max(pm, nx[u]);
+            pm = max(pm, nxt[c]);
         }
     }
     if (t == 0) ent[0] = 0;
     __syncthreads();
-    // 2. the chain from each anchor to the next
+    // 3. from each anchor, the chain to the next anchor (usually one step)
     for (int u = 0; u < CPT; ++u) {
-        const int c = t * CPT + u;
+        const int c = c0 + u;
         if (c < C && anc[c]) {
             for (int x = c;;) {
                 const int y = nxt[x];
                 if (y >= C) break;
-                ent[y] = a.link[3 * x + 2];
+                ent[y] = jx[x];
                 onc[y] = 1;
                 if (anc[y]) break;
                 x = y;
@@ -2902,47 +2987,38 @@ __global__ void __launch_bounds__(1024) resolve_kernel(ResolveArgs a)
         }
     }
     __syncthreads();
-    // 3. each chain chunk's records, trimmed to the owned range
-    auto rpb = [](long r) { return r < 0 ? r : (r & WALK_REC_PB); };
-    int cnt[CPT], fi[CPT], cb[CPT], ce[CPT];
+    // 4. each chain chunk's owned records: [entry, shared frame) trimmed to
+    // [own_lo, own_hi) (walk-in: chunk 0; past own_hi: the last chain chunk)
     long own = 0, chn = 0;
+    int cnt[RESOLVE_MAX_CHUNKS / NT], fi[RESOLVE_MAX_CHUNKS / NT];
 #pragma unroll
-    for (int u = 0; u < CPT; ++u) {
-        const int c = t * CPT + u;
-        cnt[u] = fi[u] = cb[u] = ce[u] = 0;
-        if (c < C && onc[c]) {
-            const int m = a.link[3 * c], nr = a.nrec[c];
-            const bool ovf = nr > MR;
-            int e = (m >= 0 && !ovf) ? a.link[3 * c + 1] : min(nr, MR), b = min(ent[c], e);
-            if (ovf) atomicOr(&sflags, RESOLVE_OVERFLOW);
-            cb[u] = b;
-            ce[u] = e;
-            const long* rc = a.rec + (long)c * MR;
-            if (c == 0 || m < 0 || ovf) {
-                for (int k = b; k < e; ++k)
-                    if (rpb(rc[k]) < 0) atomicOr(&sflags, RESOLVE_NEG_FRAME);
-                while (b < e && rpb(rc[b]) < a.own_lo) ++b;
-                while (e > b && rpb(rc[e - 1]) >= a.own_hi) --e;
-            }
-            if (m < 0 && !ovf) {  // the chain's last chunk: its exit state is the walk's
+    for (int u = 0; u < UP; ++u) {
+        const int c = c0 + u;
+        cnt[u] = fi[u] = 0;
+        if (u < CPT && c < C && onc[c]) {
+            const int se = sege[c], e = se & 0xffff, bt = (se >> 16) & 0x3fff;
+            if (se & SEG_OVF) atomicOr(&sflags, RESOLVE_OVERFLOW);  // its records are incomplete
+            const int b0 = ent[c], b = c == 0 ? max(b0, sfront) : b0;
+            cnt[u] = max(0, e - b);
+            fi[u] = b;
+            chn += max(0, e + bt - b0);
+            if (nxt[c] >= C) {  // the chain's last chunk: its walk's exit state is the walk's
                 sexit[0] = a.exit_pos[c];
                 sexit[1] = a.exit_ring ? a.exit_ring[c] : 0;
             }
-            cnt[u] = e - b;
-            fi[u] = b;
         }
         own += cnt[u];
-        chn += ce[u] - cb[u];
     }
     // block scan of (chain records << 32 | owned) in chunk order
-    long v = (chn << 32) | own, vi = v;
+    const long v = (chn << 32) | own;
+    long vi = v;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const long y = __shfl_up(vi, o);
         if (lane >= o) vi += y;
     }
     if (lane == 63) wsum[w] = vi;
-    __syncthreads();
+    __syncthreads();  // also: every thread is done with jx (reused for the scan)
     long off = vi - v, tot = 0;
     for (int u = 0; u < NT / 64; ++u) {
         if (u < w) off += wsum[u];
@@ -2951,22 +3027,23 @@ __global__ void __launch_bounds__(1024) resolve_kernel(ResolveArgs a)
     const long tot_own = tot & 0xffffffffL, tot_chn = tot >> 32;
     long oo = off & 0xffffffffL, oc = off >> 32;
 #pragma unroll
-    for (int u = 0; u < CPT; ++u) {
-        const int c = t * CPT + u;
-        if (c < C) {
-            excl[c] = (int)oo;
+    for (int u = 0; u < UP; ++u) {
+        const int c = c0 + u;
+        if (u < CPT && c < C) {
+            jx[c] = (int)oo;
             ent[c] = fi[u];
+            if (blockIdx.x == 0 && a.chain && onc[c]) {  // every record of the true walk (shard reports)
+                const long* rc = a.rec + (long)c * MR;
+                const int se = sege[c];
+                for (int k = c == 0 ? 0 : fi[u]; k < (se & 0xffff) + ((se >> 16) & 0x3fff); ++k, ++oc)
+                    if (oc < a.chain_cap) a.chain[oc] = rc[k];
+            }
         }
         oo += cnt[u];
-        if (blockIdx.x == 0 && a.chain) {  // every record of the true walk (shard reports)
-            const long* rc = a.rec + (long)c * MR;
-            for (int k = cb[u]; k < ce[u]; ++k, ++oc)
-                if (oc < a.chain_cap) a.chain[oc] = rc[k];
-        }
     }
     __syncthreads();
-    // 4. owned slots, spread over the workgroups: slot -> its chunk by binary
-    // search over the scan (last chunk with excl <= slot), then the record
+    // 5. owned slots, spread over the workgroups: slot -> its chunk by binary
+    // search over the scan (last chunk with scan <= slot), then the record
     const long lim = min(tot_own, a.cap);
     for (long i0 = (long)blockIdx.x * NT * G; i0 < lim; i0 += (long)gridDim.x * NT * G) {
         long pbv[G];
@@ -2979,11 +3056,11 @@ __global__ void __launch_bounds__(1024) resolve_kernel(ResolveArgs a)
             for (int it = 0; it < 14; ++it) {  // C <= 8192 = 2^13
                 const int mid = (lo + hi) >> 1;
                 const bool go = hi - lo > 1;
-                const bool le = excl[mid] <= idx;
+                const bool le = jx[mid] <= idx;
                 lo = go && le ? mid : lo;
                 hi = go && !le ? mid : hi;
             }
-            pbv[g] = rpb(a.rec[(long)lo * MR + ent[lo] + (idx - excl[lo])]);
+            pbv[g] = rpb(a.rec[(long)lo * MR + ent[lo] + (idx - jx[lo])]);
         }
 #pragma unroll
         for (int g = 0; g < G; ++g) {

@@ -150,7 +150,12 @@ struct WalkArgs {
     int lookback;
     int* pub;
     int* link;
+    // nullable diagnostics (OFDM_WALK_PROF): per chunk {start, core end,
+    // end (wall_clock64 ticks), frames past the core end, look-back polls
+    // that waited, workgroup, XCC id, frames located}
+    long* prof;
 };
+constexpr int WALK_PROF_FIELDS = 8;
 constexpr int WALK_PUB_DONE = 1 << 30;
 // a walker waits at most this many polls for the chunk it looks back on
 constexpr int WALK_SPIN_MAX = 1 << 16;
