@@ -300,7 +300,7 @@ def stream_leg(args, dist, dev, world, rank, M, i16: bool, p=None, frames_per_gp
                         "algorithmic_bytes_per_call": alg_rank, "avg_call_ms": call_ms,
                         "traffic": (pmc or {}).get("hbm_bytes_per_call")},
            "cpu_baseline": None}
-    res["compute"] = decode_compute(p, n_owned, call_ms)
+    res["compute"] = decode_compute(p, n_owned, call_ms, workload)
     if staged is not None:
         res["staged"] = staged
     if pipeline and world == 1 and args.stream_pipeline > 1:
@@ -338,18 +338,39 @@ def decode_flops_per_frame(p) -> int:
     return int(cfo + ffts + ramps + cps + emit)
 
 
-def decode_compute(p, frames: int, call_ms: float) -> dict:
-    """The decode's compute side (VALU-bound: it takes the same time with
-    int16 input at a quarter of the bytes): useful FP64 flop/s over the whole
-    call time (walker included, so a lower bound) against the FP64 vector
-    peak, and the SIMDs' VALU-busy fraction from the committed SQ counters."""
+def load_stream_kernels(workload: str):
+    """Per-kernel mean times of the stream pipeline for this workload from the
+    committed rocprofv3 kernel-trace summary (profiles/stream_kernels_*.json,
+    made by tools/stream_kernels.py), or None."""
+    import glob
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "stream_kernels_*.json"))):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if workload in d.get("workloads", {}):
+            best = dict(d["workloads"][workload], source=os.path.relpath(path, ROOT))
+    return best
+
+
+def decode_compute(p, frames: int, call_ms: float, workload: str) -> dict:
+    """The decode's compute side (VALU-bound: it takes about the same time
+    with int16 input at a quarter of the bytes): useful FP64 flop/s over the
+    decode kernel's own time (its mean launch duration in the committed
+    kernel trace of this workload) against the FP64 vector peak; over the
+    whole call time when no trace is committed (a lower bound)."""
     f = decode_flops_per_frame(p)
-    ach = f * frames / (call_ms * 1e-3) / 1e12
+    tr = load_stream_kernels(workload)
+    if tr and tr.get("decode_us"):
+        t_s, basis = tr["decode_us"] * 1e-6, f"decode kernel mean duration {tr['decode_us']:.1f} us ({tr['source']})"
+    else:
+        t_s, basis = call_ms * 1e-3, "whole call time (walk + resolve + decode): no committed trace"
+    ach = f * frames / t_s / 1e12
     return {"bound": "valu", "flops_per_frame": f, "achieved": ach, "peak": FP64_VALU_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": ach / FP64_VALU_PEAK_TFLOPS,
-            "valu_busy": 0.78 if p["fft_size"] == 512 else None,
-            "note": "flops over the whole call time (walker + decode); valu_busy of the N = 512 fused decode "
-                    "from profiles/r03l_sq_stream.txt (SQ_ACTIVE_INST_VALU / SQ_BUSY_CYCLES per SIMD)"}
+            "unit": "TFLOP/s", "frac": ach / FP64_VALU_PEAK_TFLOPS, "time_basis": basis,
+            "kernels_us": tr}
 
 
 def stream_pipelined(args, p, M, dev, modem, layout, rx, walk, outs, x, nsl, cap, i16, n_owned, exchange, SS):
