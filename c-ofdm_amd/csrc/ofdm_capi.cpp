@@ -12,6 +12,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <chrono>
 #include <cstring>
 #include <fstream>
 #include <random>
@@ -175,8 +176,9 @@ struct ofdm_ctx {
     ofdm_walk_tuning walk{};       // stream walker settings (ofdm_set_walk_tuning)
     long ring = 0;                 // rx.cpp's SDR ring R (ofdm_set_stream_ring; 0: the continuous walk)
     bool queue_zero = false;       // the last stream call's compaction left the walker counter zero
-    hipEvent_t ev_call = nullptr;  // the last stream call's work (every decode launch) is done
-    bool call_valid = false;       //   (ev_call recorded)
+    hipEvent_t ev_call = nullptr;  // recorded on call_stream when a stream call comes on another stream
+    hipStream_t call_stream = nullptr;  // the last stream call's HIP stream
+    bool call_valid = false;       //   (call_stream set)
     hipEvent_t ev_walk = nullptr;  // walk records landed in h_walk
     hipEvent_t ev_wdone = nullptr;  // the walk kernel finished (caller's stream)
     hipStream_t side = nullptr;     // copies the walk records out beside the decode
@@ -790,6 +792,7 @@ int ofdm_stream_destroy(ofdm_ctx* c, void* st)
     if (st) {
         HIP_TRY(hipStreamSynchronize((hipStream_t)st));
         rx_queue_release(c, (hipStream_t)st);
+        if (c->call_valid && c->call_stream == (hipStream_t)st) c->call_valid = false;  // drained above
         HIP_TRY(hipStreamDestroy((hipStream_t)st));
     }
     return OFDM_OK;
@@ -1501,15 +1504,22 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     // The previous stream call's work must be done before this one rewrites
     // the ctx's scratch (walk records, compacted list, channel): its decodes
     // read them. On the same stream that is stream order; on another stream
-    // this call waits for the event every stream call records on exit
-    // (header: overlapping stream calls take two contexts).
-    if (!c->ev_call) HIP_TRY(hipEventCreateWithFlags(&c->ev_call, hipEventDisableTiming));
-    if (c->call_valid) HIP_TRY(hipStreamWaitEvent(st, c->ev_call, 0));  // no-op on the same stream
-    struct CallDone {  // records ev_call after everything this call enqueues
-        ofdm_ctx* c;
-        hipStream_t st;
-        ~CallDone() { c->call_valid = hipEventRecord(c->ev_call, st) == hipSuccess; }
-    } call_done{c, st};
+    // this call waits for an event recorded now on the previous call's stream
+    // (behind that call's decodes; header: overlapping stream calls take two
+    // contexts). Recorded here rather than at the end of every call: an event
+    // between two dependent kernels of one stream costs a launch gap (the
+    // next call's walker started ~15-25 us after the decode ended).
+    if (c->call_valid && c->call_stream != st) {
+        if (!c->ev_call) HIP_TRY(hipEventCreateWithFlags(&c->ev_call, hipEventDisableTiming));
+        if (hipEventRecord(c->ev_call, c->call_stream) == hipSuccess) {
+            HIP_TRY(hipStreamWaitEvent(st, c->ev_call, 0));
+        } else {
+            (void)hipGetLastError();  // that stream is gone (destroyed): wait for the device instead
+            HIP_TRY(hipDeviceSynchronize());
+        }
+    }
+    c->call_stream = st;
+    c->call_valid = true;
     if (!c->queue_zero) HIP_TRY(hipMemsetAsync(w.queue, 0, sizeof(int), st));
     c->queue_zero = false;
     if (lbk) {
@@ -1684,10 +1694,10 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
         // into the decode's list (and pb_out), a status block to the host.
         // The decode is enqueued behind it before the host reads the status.
         const size_t ub = std::min(max_frames, (size_t)nchunks * max_rec);
-        const bool want_chain = located || nlocated_out;
-        const size_t chain_cap = want_chain ? (size_t)nchunks * max_rec : 0;
+        const bool want_chain = (located || located_lag) && located_cap > 0;
+        const size_t chain_tail = located_cap / 2, chain_head = located_cap - chain_tail;
         if ((rc = grow(c, c->s_pbs, (ub + 1) * sizeof(long))) || (rc = grow_host(c, c->h_status, 64)) ||
-            (want_chain && (rc = grow(c, c->s_chain, chain_cap * sizeof(long)))))
+            (want_chain && (rc = grow(c, c->s_chain, located_cap * sizeof(long)))))
             return rc;
         long* d_pbs = static_cast<long*>(c->s_pbs.p);
         volatile long* hs = static_cast<volatile long*>(c->h_status.p);
@@ -1700,14 +1710,17 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
         ra.exit_ring = d_exit_ring;
         ra.nchunks = nchunks;
         ra.max_rec = max_rec;
-        ra.own_lo = own_lo;
+        // a core starting at the stream's first sample also owns a frame whose
+        // preamble starts before it (rx.cpp:105-114,158: its zero header)
+        ra.own_lo = own_lo == 0 ? LONG_MIN : own_lo;
         ra.own_hi = own_hi;
         ra.cap = (long)ub;
         ra.list = d_pbs;
         ra.list2 = pb_out;
         ra.count = d_pbs + ub;
         ra.chain = want_chain ? static_cast<long*>(c->s_chain.p) : nullptr;
-        ra.chain_cap = (long)chain_cap;
+        ra.chain_head = (long)chain_head;
+        ra.chain_tail = (long)chain_tail;
         ra.status = const_cast<long*>(hs);
         ra.pub = w.pub;
         ra.queue_reset = c->d_queue;
@@ -1715,12 +1728,21 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
         if (e != hipSuccess) return hip_fail(e, "stream resolve launch");
         c->pub_zero = true;    // cleared by the resolve (stream order)
         c->queue_zero = true;  // likewise the chunk counter
-        if (!c->ev_wdone) HIP_TRY(hipEventCreateWithFlags(&c->ev_wdone, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(c->ev_wdone, st));
         const bool spec = fused && ub > 0 && ub * per <= ((size_t)256 << 20);
         if (spec && (rc = decode_fused(d_pbs, ub, d_pbs + ub))) return rc;
-        HIP_TRY(hipEventSynchronize(c->ev_wdone));
-        const long owned = hs[0], flags = hs[1], xpos = hs[2], xring = hs[3], nchain = hs[4];
+        // the resolve kernel's last word is the flags word of the status:
+        // poll it (no event between the resolve and the decode: a marker
+        // between two dependent kernels costs a launch gap); if it has not
+        // landed in 2 s, wait for the stream (errors surface there)
+        {
+            const auto t0 = std::chrono::steady_clock::now();
+            for (long spin = 0; hs[1] == -1; ++spin)
+                if ((spin & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+                    HIP_TRY(hipStreamSynchronize(st));
+                    break;
+                }
+        }
+        const long owned = hs[0], flags = hs[1], xpos = hs[2], xring = hs[3], nchain = hs[4], nneg = hs[5];
         if (flags < 0) return fail(OFDM_ERR_HIP, "stream resolve wrote no status");
         if (flags & ofdm::RESOLVE_OVERFLOW) {
             // a walker's records overflowed (a walk that met no later chunk's
@@ -1730,15 +1752,12 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
                                   nframes_out, stream, start_state, own_lo, own_hi, located, located_lag, located_cap,
                                   nlocated_out, exit_out, true);
         }
-        if (flags & ofdm::RESOLVE_NEG_FRAME)
-            return fail(OFDM_ERR_UNSUPPORTED, "a frame starts before the stream's first sample "
-                                              "(rx.cpp's ring would decode it from its zero header)");
         *nframes_out = (size_t)owned;
         if (exit_out) *exit_out = ofdm_walk_state{xpos, xpos < 0 ? 0 : xring};
+        if (nlocated_out) *nlocated_out = (size_t)nchain;
         if (want_chain) {
-            if (nlocated_out) *nlocated_out = (size_t)nchain;
-            const size_t nl = std::min({(size_t)nchain, located_cap, chain_cap});
-            if (nl && (located || located_lag)) {
+            const size_t nl = std::min((size_t)nchain, located_cap);
+            if (nl) {
                 std::vector<long> rl(nl);
                 HIP_TRY(hipMemcpy(rl.data(), c->s_chain.p, nl * sizeof(long), hipMemcpyDeviceToHost));
                 for (size_t i = 0; i < nl; ++i) {
@@ -1752,9 +1771,14 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
             fprintf(stderr, "ofdm_rx_stream: look-back, %ld chunks of %ld samples, halo %ld, %ld frames\n", nchunks,
                     chunk, halo, owned);
         const size_t nout = std::min((size_t)owned, ub);
-        if (spec || nout == 0) return OFDM_OK;
-        if (fused) return decode_fused(d_pbs, nout, nullptr);
-        return decode_gathered(d_pbs, nout);
+        // frames before sample 0 (a prefix; the fused kernels skip them): the
+        // gather path, whose samples before 0 read as zero like rx.cpp's header
+        const size_t neg = (flags & ofdm::RESOLVE_NEG_FRAME) ? std::min((size_t)nneg, nout) : 0;
+        if (spec) return neg ? decode_gathered(d_pbs, neg) : OFDM_OK;
+        if (nout == 0) return OFDM_OK;
+        if (!fused) return decode_gathered(d_pbs, nout);
+        if ((rc = decode_fused(d_pbs, nout, nullptr))) return rc;
+        return neg ? decode_gathered(d_pbs, neg) : OFDM_OK;
     }
 
     // records, exit states and counts in one copy of the walk buffer's layout
@@ -1879,9 +1903,14 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
                 lst.assign(rec + (size_t)k * max_rec, rec + (size_t)k * max_rec + nrec[k]);
             }
         }
-        if (k == 0)  // the walk-in from `start` (true by definition): frames before own_lo
-            for (long r : lst)
-                if (rec_pb(r) < lo) walk_in.push_back(r);
+        if (k == 0)  // the walk-in from `start` (true by definition): frames before own_lo; a
+            for (long r : lst) {  // core from sample 0 owns a frame before it (rx.cpp's zero header)
+                if (rec_pb(r) < lo && !(own_lo == 0 && r < 0)) walk_in.push_back(r);
+                if (own_lo == 0 && r < 0) {
+                    frames.push_back(r);
+                    owned_rec.push_back(r);
+                }
+            }
         for (long r : lst)
             if (rec_pb(r) >= lo && rec_pb(r) < hi) {
                 frames.push_back(rec_pb(r));
@@ -1892,13 +1921,6 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
         texit_ring = exr[k];
         last_k = k;
     }
-    // rx.cpp decodes a frame whose preamble the ring's zero header precedes
-    // (pb < 0: the capture starts inside a frame's preamble); the stream API's
-    // outputs index the caller's samples, so it reports the case instead
-    for (long r : walk_in)
-        if (r < 0)
-            return fail(OFDM_ERR_UNSUPPORTED, "a frame starts %ld samples before the stream's first sample "
-                                              "(rx.cpp's ring would decode it from its zero header)", -r);
     *nframes_out = frames.size();
     if (exit_out && last_k == nchunks - 1) *exit_out = ofdm_walk_state{texit, texit < 0 ? 0 : texit_ring};
     if (nlocated_out) {
@@ -1910,8 +1932,14 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
             for (long r : prev)
                 if (rec_pb(r) >= own_hi) all.push_back(r);
         *nlocated_out = all.size();
-        const size_t nl = std::min(all.size(), located_cap);
-        for (size_t i = 0; i < nl; ++i) {
+        // more than located_cap: the first located_cap - located_cap/2 and the last located_cap/2
+        if (all.size() > located_cap) {
+            const size_t tail = located_cap / 2, head = located_cap - tail;
+            std::vector<long> ht(all.begin(), all.begin() + head);
+            ht.insert(ht.end(), all.end() - tail, all.end());
+            all.swap(ht);
+        }
+        for (size_t i = 0; i < all.size(); ++i) {
             if (located) located[i] = rec_pb(all[i]);
             if (located_lag) located_lag[i] = all[i] > 0 && (all[i] & ofdm::WALK_REC_LAG) ? 1 : 0;
         }
@@ -1937,8 +1965,11 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     HIP_TRY(hipMemcpyAsync(d_pbs, c->h_frames.p, nout * sizeof(long), hipMemcpyHostToDevice, st));
     if (pb_out) HIP_TRY(hipMemcpyAsync(pb_out, d_pbs, nout * sizeof(long), hipMemcpyDeviceToDevice, st));
 
-    if (fused) return decode_fused(d_pbs, nout, nullptr);
-    return decode_gathered(d_pbs, nout);
+    if (!fused) return decode_gathered(d_pbs, nout);
+    if ((rc = decode_fused(d_pbs, nout, nullptr))) return rc;
+    size_t neg = 0;  // frames before sample 0: the gather path (the fused kernels skip them)
+    while (neg < nout && frames[neg] < 0) ++neg;
+    return neg ? decode_gathered(d_pbs, neg) : OFDM_OK;
 }
 
 extern "C" {

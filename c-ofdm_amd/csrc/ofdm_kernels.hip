@@ -559,7 +559,11 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
     const long fstep = gridDim.x;
     // frames to process: a.nframes, or fewer when the count is device-side
     // (speculative stream decode); uniform early exit before any prefetch
-    const long nfr = a.count ? min(*a.count, a.nframes) : a.nframes;
+    // stream mode: a first frame whose preamble starts before the stream's
+    // first sample is the host's (gather path, zeros before sample 0): the
+    // frames taken here are fbase, fbase + 1, ...
+    const long fbase = (SYNC && a.nframes > 0 && (!a.count || *a.count > 0) && a.starts[0] < 0) ? 1 : 0;
+    const long nfr = (a.count ? min(*a.count, a.nframes) : a.nframes) - fbase;
     // Dynamic frames (a.queue): a workgroup's first frame is its blockIdx,
     // later ones come from a counter, so workgroups that run faster (CU and
     // memory-channel placement make them differ by ~15%) take more frames and
@@ -595,7 +599,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
     for (int i = 0; i < RX_DPT; ++i) pk[i] = a.tab.rx_pack[t0 + T * i];
     const int pbin = a.tab.pilot_swz[t0];
     long fl = blockIdx.x;  // this workgroup's frame
-    auto frame_of = [&](long l) { return l; };
+    auto frame_of = [&](long l) { return l + fbase; };
     SymbolRegs<LOGN, I16> pf;
     // sample offset of frame g's first message body (CP strip, Frame.hpp:278-279)
     auto body0 = [&](long g) { return SYNC ? a.starts[g] + a.start_off : g * a.frame_stride + a.cp; };
@@ -1047,6 +1051,7 @@ __global__ void __launch_bounds__(128, 3) rx_stream2_kernel(RxArgs a)
     const int pbin = a.tab.pilot_swz[lane0];
 #pragma unroll 1
     for (long f = blockIdx.x; f < nfr; f += gridDim.x) {
+        if (a.starts[f] < 0) continue;  // uniform: before the stream's first sample (the host's gather path)
         const double2* chan = a.chan + f * a.chan_stride;
         for (int d = tid; d < D; d += 128) L.chl[d] = chan[d];
         __syncthreads();  // twiddles (first frame) and the channel visible

@@ -103,6 +103,7 @@ __global__ void __launch_bounds__(WideGeo<LOGN>::NT, 4) stream_decode_wide_kerne
 
     const long f = blockIdx.x;
     if (a.count && f >= *a.count) return;  // uniform: past the speculative frame count
+    if (a.starts[f] < 0) return;           // before the stream's first sample: the host's gather path
     int tid;
     asm volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"((int)threadIdx.x));
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;

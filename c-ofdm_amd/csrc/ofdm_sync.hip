@@ -411,6 +411,10 @@ __global__ void __launch_bounds__(G * (1 << LOGM) / 8) cfo_kernel(CfoArgs a)
     const int tid = threadIdx.x, g = tid / T, t = tid - g * T;
     const long f = blockIdx.x;
     if (a.count && f >= *a.count) return;  // uniform: past the speculative frame count
+    // a stream frame whose preamble starts before the stream's first sample
+    // (rx.cpp decodes it from its ring's zero header) is decoded by the
+    // host's gather path, which reads those samples as zero
+    if (a.starts && a.starts[f] < 0) return;
     const long x0 = a.starts ? a.starts[f] : f * a.frame_stride;
     // the combine twiddles are requested before the samples (in-order
     // vector-memory returns: issued after them they would wait behind every
@@ -933,6 +937,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 3) stream_params_kernel(Strea
     const int t = threadIdx.x;
     const long f = blockIdx.x;
     if (a.count && f >= *a.count) return;  // uniform: past the speculative frame count
+    if (a.starts[f] < 0) return;           // before the stream's first sample: the gather path's
     const long x0 = a.starts[f];
     const double cfo = a.cfo[f];
     const int L = N + a.cp, half = a.D / 2, Q = 1 + a.S, LT = L / T, CT = a.cp / T;
@@ -1654,6 +1659,7 @@ __global__ void __launch_bounds__(128, 4) stream_decode_kernel(CfoArgs c, Stream
     const int lane0 = threadIdx.x & 63;
     const long f = blockIdx.x;
     if (a.count && f >= *a.count) return;  // uniform: past the speculative frame count
+    if (a.starts[f] < 0) return;           // before the stream's first sample: the gather path's
     // one frame per workgroup (a persistent frame loop let the compiler hoist
     // the sync stage's math-library constants and tables out of it: spills)
     int pk[RX_DPT];
@@ -2888,7 +2894,7 @@ __global__ void __launch_bounds__(1024) resolve_kernel(ResolveArgs a)
     __shared__ unsigned char anc[NC], onc[NC];
     __shared__ long wsum[NT / 64];
     __shared__ int wmax[NT / 64];
-    __shared__ int sflags, sfront;
+    __shared__ int sflags, sfront, sneg;
     __shared__ long sexit[2];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int C = (int)a.nchunks, MR = a.max_rec;
@@ -2896,6 +2902,7 @@ __global__ void __launch_bounds__(1024) resolve_kernel(ResolveArgs a)
     if (t == 0) {
         sflags = 0;
         sfront = 0;
+        sneg = 0;
         sexit[0] = -1;
         sexit[1] = 0;
     }
@@ -2926,10 +2933,14 @@ __global__ void __launch_bounds__(1024) resolve_kernel(ResolveArgs a)
             long r[TR];
 #pragma unroll
             for (int k = 0; k < TR; ++k) r[k] = rc[min(k, max(e - 1, 0))];
-            int f = 0;
-            if (e > 0 && rpb(r[0]) < 0) atomicOr(&sflags, RESOLVE_NEG_FRAME);
+            int f = 0, ng = 0;
 #pragma unroll
-            for (int k = 0; k < TR; ++k) f += (k < e && rpb(r[k]) < a.own_lo) ? 1 : 0;
+            for (int k = 0; k < TR; ++k) {
+                f += (k < e && rpb(r[k]) < a.own_lo) ? 1 : 0;
+                ng += (k < e && rpb(r[k]) >= a.own_lo && rpb(r[k]) < 0) ? 1 : 0;
+            }
+            sneg = ng;  // owned frames before the stream's first sample (a prefix of the list)
+            if (ng) atomicOr(&sflags, RESOLVE_NEG_FRAME);
             while (f >= TR && f < e && rpb(rc[f]) < a.own_lo) ++f;  // longer walk-ins (rare)
             sfront = f;
         }
@@ -3032,11 +3043,23 @@ __global__ void __launch_bounds__(1024) resolve_kernel(ResolveArgs a)
         if (u < CPT && c < C) {
             jx[c] = (int)oo;
             ent[c] = fi[u];
-            if (blockIdx.x == 0 && a.chain && onc[c]) {  // every record of the true walk (shard reports)
+            if (blockIdx.x == 0 && a.chain && onc[c]) {
+                // the walk's first chain_head and last chain_tail records
+                // (shard reports): chain index q goes to q (head) or to
+                // chain_head + q - (tot - chain_tail) (tail); only the
+                // chunks holding those write
                 const long* rc = a.rec + (long)c * MR;
-                const int se = sege[c];
-                for (int k = c == 0 ? 0 : fi[u]; k < (se & 0xffff) + ((se >> 16) & 0x3fff); ++k, ++oc)
-                    if (oc < a.chain_cap) a.chain[oc] = rc[k];
+                const int se = sege[c], kb = c == 0 ? 0 : fi[u], ke = (se & 0xffff) + ((se >> 16) & 0x3fff);
+                const long tl = max(a.chain_head, tot_chn - a.chain_tail);  // first tail index
+                for (int k = kb; k < ke; ++k, ++oc) {
+                    if (oc < a.chain_head) a.chain[oc] = rc[k];
+                    else if (oc >= tl) a.chain[a.chain_head + (oc - tl)] = rc[k];
+                    else {  // skip the middle of this chunk's run
+                        const long skip = min((long)(ke - k), tl - oc) - 1;
+                        k += (int)skip;
+                        oc += skip;
+                    }
+                }
             }
         }
         oo += cnt[u];
@@ -3077,11 +3100,16 @@ __global__ void __launch_bounds__(1024) resolve_kernel(ResolveArgs a)
         if (t == 0) {
             *a.count = tot_own;
             if (a.queue_reset) *a.queue_reset = 0;
+            // page-locked status the host polls: the fields, a system-scope
+            // release, then the flags word it waits on (-1 until then)
             a.status[0] = tot_own;
-            a.status[1] = sflags;
             a.status[2] = sexit[0];
             a.status[3] = sexit[1];
             a.status[4] = tot_chn;
+            a.status[5] = sneg;
+            __threadfence_system();
+            __hip_atomic_store(a.status + 1, (long)sflags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __threadfence_system();
         }
     }
 }

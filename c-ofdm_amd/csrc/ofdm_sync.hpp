@@ -238,14 +238,16 @@ struct ResolveArgs {
     const long* exit_ring;      // [chunk] (nullable: ring off)
     long nchunks;
     int max_rec;
-    long own_lo, own_hi;        // owned preamble starts; own_lo = LONG_MIN: no lower bound
+    long own_lo, own_hi;        // owned preamble starts; own_lo = LONG_MIN: no lower bound (whole stream:
+                                //   a frame before sample 0 is the stream's, as rx.cpp decodes it)
     long cap;                   // list capacity
     long* list;                 // owned preamble starts
     long* list2;                // nullable: a second copy (the caller's pb_out)
     long* count;                // owned frames (uncapped)
-    long* chain;                // nullable: every record of the true walk
-    long chain_cap;
-    long* status;               // {owned, flags (RESOLVE_*), exit pos, exit ring end, chain records}
+    long* chain;                // nullable: records of the true walk: the first chain_head, then the
+    long chain_head, chain_tail;  //   last chain_tail (all of them, in order, when they are fewer)
+    long* status;               // {owned, flags (RESOLVE_*), exit pos, exit ring end, chain records,
+                                //  owned frames before sample 0 (a prefix of the list)}
     int* pub;                   // zeroed for the next call
     int* queue_reset;           // nullable: the walkers' chunk counter, zeroed
 };

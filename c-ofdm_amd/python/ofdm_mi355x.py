@@ -407,7 +407,10 @@ class Modem:
         """ofdm_rx_stream_shard: the walk from state `start` = (pos, ring_end)
         over this shard's n samples, frames with pb in [own_lo, own_hi)
         decoded. Returns (frames decoded, located pbs (numpy int64, relative),
-        their ring lags (numpy uint8), exit state (pos, ring_end))."""
+        their ring lags (numpy uint8), exit state (pos, ring_end)); when the
+        walk located more than located_cap frames, the located arrays hold
+        the first located_cap - located_cap // 2 and the last located_cap // 2
+        of them (located_cap = 0: no list, empty arrays)."""
         import numpy as np
         m, nl, ex = C.c_size_t(), C.c_size_t(), WalkState()
         cap = max(1, located_cap)
@@ -416,14 +419,14 @@ class Modem:
             self._located_lag = np.empty(cap, dtype=np.uint8)
         loc, lag = self._located, self._located_lag
         st = WalkState(*start)
+        want = located_cap > 0
         check(lib().ofdm_rx_stream_shard(self.h, None if i16 else _ptr(iq), _ptr(iq) if i16 else None, n,
                                          C.byref(st), own_lo, own_hi, max_frames, chunk, _ptr(pb_out),
                                          _ptr(bytes_out), _ptr(constell_out), _ptr(cfo_out), C.byref(m),
-                                         loc.ctypes.data, lag.ctypes.data, located_cap, C.byref(nl), C.byref(ex),
-                                         _stream(stream)))
-        if nl.value > located_cap:
-            raise OfdmError(-1, f"located list of {nl.value} frames exceeds located_cap={located_cap}")
-        return m.value, loc[:nl.value].copy(), lag[:nl.value].copy(), (ex.pos, ex.ring_end)
+                                         loc.ctypes.data if want else None, lag.ctypes.data if want else None,
+                                         located_cap, C.byref(nl), C.byref(ex), _stream(stream)))
+        k = min(nl.value, located_cap)
+        return m.value, loc[:k].copy(), lag[:k].copy(), (ex.pos, ex.ring_end)
 
     def sync_frames(self, frames, nframes: int, frame_stride: int, stages: int = SYNC_ALL,
                     cfo_in=None, cfo_out=None, chan_out=None, stream=None):

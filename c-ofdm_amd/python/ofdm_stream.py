@@ -228,9 +228,14 @@ class ShardedStreamRx:
     def run(self, walk, exchange) -> int:
         """The walk, the report exchange and any re-walks; returns this rank's
         owned frame count (its outputs hold them, in stream order)."""
-        rep = self.first_walk(walk)
-        if self.world == 1:  # the walk from the stream's initial state is the true walk
+        if self.world == 1:  # the walk from the stream's initial state is the true walk: no report
+            quiet = getattr(walk, "no_report", None)
+            if quiet is not None:
+                self.n_owned = quiet(self._rel(self.initial))
+                return self.n_owned
+            self.first_walk(walk)
             return self.n_owned
+        rep = self.first_walk(walk)
         while True:
             rows = exchange(pack_report(rep, self.cap))
             reps = [unpack_report(np.asarray(r), self.cap) for r in rows]
@@ -284,11 +289,18 @@ def torch_exchange(dist, device):
 
 
 def hip_walker(modem, x_slice, n_slice: int, own_lo_rel: int, own_hi_rel: int, max_frames: int, outputs: dict,
-               i16: bool = False, chunk: int = 0, stream=None):
+               i16: bool = False, chunk: int = 0, stream=None, report_cap: int = 64):
     """walk(start_rel) over one rank's device-resident slice through
     ofdm_rx_stream_shard; outputs: pb_out / bytes_out / constell_out / cfo_out
-    device tensors for max_frames frames (pb relative to the slice)."""
+    device tensors for max_frames frames (pb relative to the slice). The
+    located list holds the walk's first and last report_cap frames (all a
+    report packs, pack_report); walk.no_report(start_rel) skips it (one rank)."""
     def walk(start_rel):
         return modem.rx_stream_shard(x_slice, n_slice, start_rel, own_lo_rel, own_hi_rel, max_frames,
-                                     chunk=chunk, i16=i16, located_cap=max_frames + 256, stream=stream, **outputs)
+                                     chunk=chunk, i16=i16, located_cap=2 * report_cap, stream=stream, **outputs)
+
+    def no_report(start_rel):  # one rank: the owned frames only, no located list
+        return modem.rx_stream_shard(x_slice, n_slice, start_rel, own_lo_rel, own_hi_rel, max_frames,
+                                     chunk=chunk, i16=i16, located_cap=0, stream=stream, **outputs)[0]
+    walk.no_report = no_report
     return walk

@@ -351,7 +351,10 @@ int ofdm_sync_frames(ofdm_ctx* ctx, double* frames, size_t nframes, size_t frame
  * as rx.cpp does, at the zero header before it (ofdm_stream_initial_state);
  * samples past n read as zero (the walk ends once its scan passes n).
  * A frame the walk locates past the stream end stops the walk. A frame whose
- * preamble would start before sample 0 fails with OFDM_ERR_UNSUPPORTED.
+ * preamble starts before sample 0 (a capture that begins inside it; rx.cpp
+ * locates it in its ring's zero header, rx.cpp:105-114,158) is decoded as
+ * rx.cpp decodes it, with the samples before 0 read as zero; its pb_out
+ * entry is negative.
  * The walk runs as parallel chunk walkers joined into the one sequential
  * walk on the device (chunk = samples per walker, 0 = automatic; see
  * ofdm_walk_tuning). Outputs (device, nullable):
@@ -405,10 +408,14 @@ int ofdm_stream_initial_state(const ofdm_ctx* ctx, ofdm_walk_state* out);
  *     located the first frame past own_hi), pos -1 if the samples ran out.
  *   located (host, nullable, located_cap entries) / located_lag (host,
  *     nullable: ring mode's state after the frame has the later of its two
- *     possible ring ends) / *nlocated_out (nullable): every frame the walk
+ *     possible ring ends) / *nlocated_out (nullable): the frames the walk
  *     located from `start` until it stopped: those before own_lo, the owned
- *     ones, and any located past own_hi. Two walks that located the same
- *     frame with the same lag are in the same state from there on.
+ *     ones, and any located past own_hi; *nlocated_out counts them all, and
+ *     when they are more than located_cap the arrays hold the first
+ *     located_cap - located_cap/2 and the last located_cap/2 of them (what a
+ *     shard-to-shard check reads: the walk-in and the frames past own_hi).
+ *     Two walks that located the same frame with the same lag are in the
+ *     same state from there on. located_cap = 0: no list is made.
  * ofdm_rx_stream(iq, n) is ofdm_rx_stream_shard(iq, n, initial state, 0, n). */
 int ofdm_rx_stream_shard(ofdm_ctx* ctx, const double* iq, const int16_t* iq16, size_t n,
                          const ofdm_walk_state* start, long own_lo, long own_hi, size_t max_frames, long chunk,

@@ -75,6 +75,16 @@ def want_walk(cfg, x, ring=None):
     return O.stream_walk_ring(cfg, x, ring=ring)[0]
 
 
+def frame_at(x, pb, span):
+    """Samples [pb, pb + span) of the stream, zero before sample 0 (rx.cpp's
+    ring header, rx.cpp:105-114) and past its end."""
+    out = np.zeros(span, np.complex128)
+    lo, hi = max(pb, 0), min(pb + span, len(x))
+    if hi > lo:
+        out[lo - pb:hi - pb] = x[lo:hi]
+    return out
+
+
 def check_against_oracle(cfg, x, got, ring=None):
     nf, pbs, out, cons, cfo = got
     want = want_walk(cfg, x, ring)
@@ -83,7 +93,7 @@ def check_against_oracle(cfg, x, got, ring=None):
     g = O.geometry(cfg)
     span = g["preamble_len"] + g["message_len"]
     for f, pb in enumerate(want):
-        c, oc, ob = O.decode_frame(cfg, x[pb: pb + span])
+        c, oc, ob = O.decode_frame(cfg, frame_at(x, pb, span))
         assert cfo[f] == c
         assert rel_err(cons[f], oc) < 1e-9
         assert np.array_equal(out[f], ob)
@@ -348,17 +358,27 @@ def test_stream_edges():
     cut = want[-1] + g["preamble_len"] + g["message_len"] - 1
     nf2, pbs2, *_ = run_stream(D, x[:cut])
     assert np.array_equal(pbs2, want_walk(D, x[:cut])) and nf2 == len(want) - 1
-    # ring mode: a capture that starts inside a frame's preamble would have
-    # rx.cpp decode from its zero header; the stream API reports it (or, if
-    # the walk does not lock there, simply starts later), never reads before 0
-    for cut0 in (g["frame_len"] // 2, 300, 40, 0):
-        y = x[max(0, want[0] - cut0):]
-        w = want_walk(D, y)
-        if len(w) and w[0] < 0:
-            with pytest.raises(M.OfdmError, match="before the stream"):
-                run_stream(D, y)
-        else:
-            assert np.array_equal(run_stream(D, y)[1], w)
+
+
+
+@pytest.mark.parametrize("lookback", [1, 0], ids=["lookback", "host_stitch"])
+@pytest.mark.parametrize("cut0", [3000, 700, 300, 120, 64, 1, 0, -1, -64, -200, -700, -3000])
+def test_stream_capture_starting_inside_a_frame(cut0, lookback):
+    # ring mode: a capture that starts cut0 samples before the first frame's
+    # preamble start (inside its T2 marker for 0 < cut0 <= T2sin_size; inside
+    # its preamble or message for cut0 < 0). rx.cpp walks from its ring's
+    # zero header (rx.cpp:105-114), and a preamble search (rx.cpp:158-168)
+    # that finds none moves on by a message; one that finds a preamble in the
+    # header region (pb < 0) decodes that frame from the zeros. The stream API
+    # locates the frames rx.cpp's loop replayed on a real ring buffer locates
+    # (orc_rx_app_walk), and decodes each as the oracle does on the same
+    # samples (zero before sample 0)
+    x, _ = impaired_stream(D, 10, seed=21)
+    first = int(want_walk(D, x)[0])
+    y = x[max(0, first - cut0):]
+    w = want_walk(D, y)
+    assert np.array_equal(w, O.rx_app_walk(D, y))  # the state form is rx.cpp's loop
+    check_against_oracle(D, y, run_stream(D, y, tuning=dict(lookback=lookback)))
 
 
 def to_i16(x):
