@@ -2,6 +2,7 @@
 // boundary). Host side: config parsing, validation, the constant tables the
 // reference builds in its constructors, and kernel dispatch. Every compute
 // entry point launches HIP kernels; there is no CPU compute path.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -13,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <chrono>
+#include <mutex>
 #include <cstring>
 #include <fstream>
 #include <random>
@@ -2063,6 +2065,74 @@ int ofdm_set_stream_ring(ofdm_ctx* c, long ring)
         return fail(OFDM_ERR_INVALID, "ring must be 0 or at least output_size (rx.cpp's buffer holds output_size + R, "
                                       "R = rx_buf_size * output_size)");
     c->ring = ring;
+    return OFDM_OK;
+}
+
+int ofdm_shard_range(size_t total, int world, int rank, size_t* first, size_t* count)
+{
+    if (world < 1 || rank < 0 || rank >= world || !first || !count)
+        return fail(OFDM_ERR_INVALID, "need world >= 1, 0 <= rank < world and non-null outputs");
+    const size_t base = total / (size_t)world, rem = total % (size_t)world;
+    *count = base + ((size_t)rank < rem ? 1 : 0);
+    *first = (size_t)rank * base + std::min((size_t)rank, rem);
+    return OFDM_OK;
+}
+
+int ofdm_stream_shard_plan(const ofdm_params* p, size_t n, int world, int rank, long* slice_lo, long* slice_hi,
+                           long* own_lo, long* own_hi)
+{
+    if (!p || !slice_lo || !slice_hi || !own_lo || !own_hi) return fail(OFDM_ERR_INVALID, "null argument");
+    size_t first = 0, count = 0;
+    int rc = ofdm_shard_range(n, world, rank, &first, &count);
+    if (rc) return rc;
+    // ofdm_stream.py: stream_halo / stream_tail (the library's shard margins)
+    const long L = p->fft_size + p->cp_size, t2 = p->t2sin_size, pre = L * p->num_pr_symb, msg = L * p->num_symb;
+    const long flen = t2 + pre + msg, window = 2 * t2 + p->pr_sin_len;
+    const long halo = std::max(3 * flen, flen + window + t2);
+    const long tail = ofdm::WALK_SCAN_MAX + t2 + window + pre + msg + 1;
+    *own_lo = (long)first;
+    *own_hi = (long)(first + count);
+    *slice_lo = std::max(0L, *own_lo - halo);
+    *slice_hi = std::min((long)n, *own_hi + tail);
+    return OFDM_OK;
+}
+
+int ofdm_reduce_counters(ofdm_ctx* c, int64_t* counters, size_t count, void* comm, void* stream)
+{
+    if (!c || !counters || !comm) return fail(OFDM_ERR_INVALID, "null argument");
+    // RCCL is loaded on first use (the core library does not link it): the
+    // one collective of a multi-GPU job, ncclAllReduce(int64, sum)
+    using AllReduce = int (*)(const void*, void*, size_t, int, int, void*, hipStream_t);
+    using ErrStr = const char* (*)(int);
+    static std::mutex mu;
+    static AllReduce all_reduce = nullptr;
+    static ErrStr err_str = nullptr;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        if (!all_reduce) {
+            void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+            if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+            if (!h) return fail(OFDM_ERR_UNSUPPORTED, "RCCL (librccl.so) not found: %s", dlerror());
+            all_reduce = reinterpret_cast<AllReduce>(dlsym(h, "ncclAllReduce"));
+            err_str = reinterpret_cast<ErrStr>(dlsym(h, "ncclGetErrorString"));
+            if (!all_reduce) return fail(OFDM_ERR_UNSUPPORTED, "librccl.so has no ncclAllReduce");
+        }
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    constexpr int kInt64 = 4, kSum = 0;  // rccl.h: ncclInt64, ncclSum
+    const int r = all_reduce(counters, counters, count, kInt64, kSum, comm, (hipStream_t)stream);
+    if (r != 0) return fail(OFDM_ERR_HIP, "ncclAllReduce: %s", err_str ? err_str(r) : "error");
+    return OFDM_OK;
+}
+
+int ofdm_device_count(int* count)
+{
+    if (!count) return fail(OFDM_ERR_INVALID, "null argument");
+    *count = 0;
+    int n = 0;
+    const hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
+    *count = n;
     return OFDM_OK;
 }
 

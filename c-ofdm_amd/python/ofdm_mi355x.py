@@ -135,6 +135,10 @@ SIGNATURES = {
     "ofdm_walk_tuning_default": (_I, [C.POINTER(WalkTuning)]),
     "ofdm_get_walk_tuning": (_I, [_V, C.POINTER(WalkTuning)]),
     "ofdm_set_walk_tuning": (_I, [_V, C.POINTER(WalkTuning)]),
+    "ofdm_shard_range": (_I, [_SZ, _I, _I, C.POINTER(_SZ), C.POINTER(_SZ)]),
+    "ofdm_stream_shard_plan": (_I, [_PP, _SZ, _I, _I, C.POINTER(_L), C.POINTER(_L), C.POINTER(_L), C.POINTER(_L)]),
+    "ofdm_reduce_counters": (_I, [_V, _V, _SZ, _V, _V]),
+    "ofdm_device_count": (_I, [C.POINTER(_I)]),
 }
 
 _lib = None

@@ -430,6 +430,33 @@ int ofdm_rx_stream_shard(ofdm_ctx* ctx, const double* iq, const int16_t* iq16, s
  * window, then the frame). Either pointer may be NULL. */
 int ofdm_stream_shard_margins(const ofdm_ctx* ctx, long* halo_out, long* tail_out);
 
+/* ---- multi-GPU (BASELINE configs[4]) -------------------------
+ * One process (or thread) per GPU, one ofdm_ctx per GPU. Frames are
+ * independent, so a batch shards as contiguous frame ranges with no data-path
+ * collective; the job's one collective is a SUM all-reduce of its counters
+ * (bit errors, bits, samples, frames) over RCCL (xGMI). A stream shards by
+ * samples: each rank walks its core plus a walk-in halo and a tail, and the
+ * ranks check their walks against each other with one small exchange
+ * (c-ofdm_amd/python/ofdm_stream.py; ofdm_rx_stream_shard). See
+ * INTEGRATION.md for the 8-GPU C++ binding (apps/ofdm_multigpu.cpp). */
+/* Contiguous share of `total` units for `rank` of `world`, the remainder to
+ * the low ranks: [*first, *first + *count). */
+int ofdm_shard_range(size_t total, int world, int rank, size_t* first, size_t* count);
+/* A stream of n samples sharded by samples: `rank`'s core [*own_lo, *own_hi)
+ * and the slice [*slice_lo, *slice_hi) it must hold (the core plus a 3-frame
+ * walk-in halo, at least ofdm_stream_shard_margins' halo, and the tail a walk
+ * crossing own_hi reads), clipped to [0, n). The plan of ofdm_stream.py's
+ * shard_stream. Pure arithmetic on the config: no GPU needed. */
+int ofdm_stream_shard_plan(const ofdm_params* params, size_t n, int world, int rank, long* slice_lo,
+                           long* slice_hi, long* own_lo, long* own_hi);
+/* The job's one collective: SUM all-reduce, in place, of `count` int64
+ * counters in device memory over an RCCL communicator (ncclComm_t passed as
+ * void*; every rank calls it), enqueued on `stream`. RCCL (librccl.so) is
+ * loaded at the first call; without it OFDM_ERR_UNSUPPORTED. */
+int ofdm_reduce_counters(ofdm_ctx* ctx, int64_t* counters, size_t count, void* nccl_comm, void* stream);
+/* Visible HIP devices (0 and OFDM_ERR_HIP without a GPU). */
+int ofdm_device_count(int* count);
+
 /* ---- stream walk tuning (tests and experiments) --------------------------
  * Per-context settings of the ofdm_rx_stream* walkers; ofdm_create sets the
  * defaults (ofdm_walk_tuning_default), which are the product configuration.

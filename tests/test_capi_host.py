@@ -108,3 +108,47 @@ def test_reference_apps_build_unchanged_against_compat_headers():
         assert os.access(path, os.X_OK)
         ldd = subprocess.run(["ldd", path], capture_output=True, text=True).stdout
         assert "libofdm_compat.so" in ldd and "not found" not in ldd
+
+
+def test_shard_range_and_stream_plan_match_python_sharding():
+    """The multi-GPU C-ABI (ofdm_shard_range, ofdm_stream_shard_plan) gives
+    the frame and stream shards the Python launcher uses (ofdm_dist.shard,
+    ofdm_stream.shard_stream with its halo / tail): no GPU needed."""
+    import ofdm_dist
+    import ofdm_stream as SS
+    L = M.lib()
+    first, count = C.c_size_t(), C.c_size_t()
+    for total in (0, 1, 7, 8192, 30517, 10 ** 9 + 3):
+        for world in (1, 2, 3, 4, 8):
+            got = []
+            for r in range(world):
+                assert L.ofdm_shard_range(total, world, r, C.byref(first), C.byref(count)) == 0
+                assert (first.value, count.value) == ofdm_dist.shard(total, world, r)
+                got.append((first.value, count.value))
+            assert sum(c for _, c in got) == total
+    assert L.ofdm_shard_range(10, 2, 2, C.byref(first), C.byref(count)) != 0  # rank out of range
+    for name, cfg in (("D", O.DEFAULT), ("B", O.CONFIG_B)):
+        p = M.Params.make(**cfg)
+        halo, tail = SS.stream_halo(cfg), SS.stream_tail(cfg)
+        v = [C.c_long() for _ in range(4)]
+        for n in (10 ** 6, 132_314_816):
+            for world in (1, 2, 4, 8):
+                for r in range(world):
+                    assert L.ofdm_stream_shard_plan(C.byref(p), n, world, r, *[C.byref(x) for x in v]) == 0
+                    assert tuple(x.value for x in v) == SS.shard_stream(n, world, r, halo, tail), (name, n, world, r)
+
+
+def test_multigpu_app_plan_only():
+    """apps/ofdm_multigpu.cpp --plan-only: the C++ job's shard plan without a GPU."""
+    import json
+    import subprocess
+    import ofdm_dist
+    app = os.path.join(os.path.dirname(M.HEADER), "..", "c-ofdm_amd", "bin", "ofdm_multigpu")
+    if not os.path.exists(app):
+        pytest.skip("ofdm_multigpu not built")
+    out = subprocess.run([app, "--plan-only", "--gpus", "8", "--total-frames", "30517"], capture_output=True,
+                         text=True, timeout=60, check=True).stdout
+    d = json.loads(out)
+    assert d["world"] == 8 and len(d["ranks"]) == 8
+    for r in d["ranks"]:
+        assert (r["first"], r["count"]) == ofdm_dist.shard(30517, 8, r["rank"])
