@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 5: kernel trace of bench.py's stream legs (serial calls): per-call
+# kernel trace of bench.py's stream legs (serial calls): per-call
 # walker / resolve / decode times and the gaps between them; and per-workload
 # kernel means of stream_bench.py (profiles/stream_kernels_*.json)
 export TMPDIR=/tmp

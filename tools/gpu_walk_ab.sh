@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 5: the look-back walk (device-side stitching, no walk-in halo) against
+# the look-back walk (device-side stitching, no walk-in halo) against
 # the round-4 halo walk with host stitching (walk tuning lookback=0), same box:
 # per-kernel mean times from rocprofv3 --kernel-trace --stats of stream_bench.py
 export TMPDIR=/tmp

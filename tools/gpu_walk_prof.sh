@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 5: walker timelines (OFDM_WALK_PROF) of stream_bench.py calls, f64 / int16,
+# walker timelines (OFDM_WALK_PROF) of stream_bench.py calls, f64 / int16,
 # look-back with 1 and 2 chunks per slot and the halo walk
 export TMPDIR=/tmp
 mkdir -p gpurun_out

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 5: look-back walker tuning sweep (chunks per walker slot x walk-in
+# look-back walker tuning sweep (chunks per walker slot x walk-in
 # halo) on stream_bench.py, per-kernel means from rocprofv3 --stats; the
 # stream parity tests first
 export TMPDIR=/tmp
