@@ -1,6 +1,6 @@
 // ofdm_stream_wide.hip — the fused stream decode for the wide geometries:
-// N = 2048 and 4096 with cp = N/4 (BASELINE configs B and C), whose
-// pilot_freq_sinh form is 5 x N/4 points. The N = 512 geometry (config D)
+// N = 1024, 2048 and 4096 with cp = N/4 (BASELINE configs B and C at 2048 /
+// 4096), whose pilot_freq_sinh form is 5 x N/4 points. The N = 512 geometry (config D)
 // has its own kernel (ofdm_sync.hip stream_decode_kernel), whose one-wave
 // transforms do not scale to these sizes.
 //
@@ -55,13 +55,14 @@ struct WideGeo {
     static constexpr int NB = LOGN - 6;            // bits of lq / 8 (lq < T)
     static constexpr int RTS = 8 + NB + 1;         // ramp table entries per message symbol
     static_assert(M == NT, "one combine bin per thread");
-    static_assert(TM % 64 == 0, "CFO transforms of whole waves");
+    static_assert(TM % 64 == 0 || 64 % TM == 0, "CFO transforms of whole waves, or several per wave");
     static_assert(LT == 10 && CT == 2, "cp = N/4");
 };
 
 // The sync stage's arrays, in the upper quarter of the two-image region
 // (image 1's half: free until the rx stage), after the CFO transforms
-// [0, 5N/4), dat [5N/4, 3N/2) and ph [3N/2, 13N/8 + 1).
+// [0, 5N/4), dat [5N/4, 3N/2) and ph [3N/2, 13N/8 + 1). At N = 1024 they run
+// ~85 entries past the images: REGION is what the kernel reserves.
 template <int LOGN>
 struct WideSyncLds {
     using W = WideGeo<LOGN>;
@@ -73,7 +74,7 @@ struct WideSyncLds {
     static constexpr int PSI = PHI + 32;                    // 64 doubles
     static constexpr int WSUM = PSI + 32;                   // T + 2 ints
     static constexpr int END = WSUM + (W::T + 2 + 3) / 4;
-    static_assert(END <= 2 * W::N, "sync arrays inside the image region");
+    static constexpr int REGION = END > 2 * W::N ? (END + 7) / 8 * 8 : 2 * W::N;  // images + sync arrays
 };
 
 template <int LOGN, bool I16>
@@ -88,8 +89,8 @@ __global__ void __launch_bounds__(WideGeo<LOGN>::NT, 4) stream_decode_wide_kerne
     extern __shared__ double2 smem[];
     const int S = a.S, D = a.D, P = a.P, half = D / 2, Q = 1 + S;
     double2* tw = smem;
-    double2* A = tw + TwLds<LOGN>::SIZE;  // 2N: the two transform images
-    double2* pil = A + 2 * N;             // S*P raw pilots (rx stage)
+    double2* A = tw + TwLds<LOGN>::SIZE;  // 2N: the two transform images (+ the sync arrays' overhang)
+    double2* pil = A + SL::REGION;        // S*P raw pilots (rx stage)
     double2* rtg = pil + S * P;           // the ramp table (sync -> rx), then the gains
     double2* misc = rtg + (S * P > RTS * S ? S * P : RTS * S);  // {b, aa}, e^{-i phi_pr}
     double2* dat = A + 5 * M;
@@ -113,8 +114,11 @@ __global__ void __launch_bounds__(WideGeo<LOGN>::NT, 4) stream_decode_wide_kerne
     // The CFO transforms occupy the first CFO_W waves; the others meanwhile
     // sum the CP correlations (cp_freq_sinh's raw sums need no CFO: the
     // rotation by e^{-2 pi i cfo N} is applied to the sum afterwards).
-    constexpr int CFO_W = G * TM / 64;
+    // (TM < 64: 64/TM transforms per wave, the last wave's spare lanes run a
+    // dummy transform into the free LDS past the five)
+    constexpr int CFO_W = (G * TM + 63) / 64;
     static_assert(CFO_W < NW, "waves left for the CP sums");
+    static_assert(CFO_W * 64 / TM * M <= 3 * N / 2, "the dummy transforms stay below ph");
     __builtin_amdgcn_s_setprio(1);  // the sync stage's chains ahead of the other frame's transforms
     {
         // the combine twiddles first (in-order vector-memory returns)
@@ -131,10 +135,11 @@ __global__ void __launch_bounds__(WideGeo<LOGN>::NT, 4) stream_decode_wide_kerne
             for (int i = 0; i < 8; ++i) v[i] = src_sample_t<I16>(c.x, c.x16, x0 + (long)G * (tt + TM * i) + g);
         }
         load_twiddles<LOGN>(a.tab.tw, tw, tid, NT);
-        if constexpr (TM == 64) {
-            // one wave per transform: each CFO wave writes the whole M-point
-            // table itself (the same values at the same addresses), so its own
-            // LDS wait publishes it, and the transforms sync within their wave
+        if constexpr (TM <= 64) {
+            // one wave per transform (64/TM per wave at N = 1024): each CFO
+            // wave writes the whole M-point table itself (the same values at
+            // the same addresses), so its own LDS wait publishes it, and the
+            // transforms sync within their wave
             if (act) {
                 load_twiddles<LOGM>(c.tw_sub, twm, lane, 64);
                 wave_lds_sync();
@@ -161,7 +166,7 @@ __global__ void __launch_bounds__(WideGeo<LOGN>::NT, 4) stream_decode_wide_kerne
                 if (lane == 0) cps[q] = acc;
             }
         }
-        if constexpr (TM == 64)
+        if constexpr (TM <= 64)
             __syncthreads();  // the transforms and the CP sums visible
         else
             fft_block_active<LOGM, -1>(v, tt, twm, A + (act ? g : 0) * M, act);
@@ -584,7 +589,7 @@ static size_t wide_shm(const StreamParamsArgs& a)
 {
     using W = WideGeo<LOGN>;
     const size_t sp = (size_t)a.S * a.P, rt = (size_t)W::RTS * a.S;
-    return sizeof(double2) * (TwLds<LOGN>::SIZE + 2 * (size_t)W::N + sp + std::max(sp, rt) + 2);
+    return sizeof(double2) * (TwLds<LOGN>::SIZE + (size_t)WideSyncLds<LOGN>::REGION + sp + std::max(sp, rt) + 2);
 }
 
 template <int LOGN, bool I16>
@@ -600,17 +605,18 @@ static hipError_t wide_launch(const CfoArgs& c, const StreamParamsArgs& a, const
 
 bool stream_decode_wide_fits(const StreamParamsArgs& a, int logn, int logm, int g, int cfo_p)
 {
-    if (logn != 11 && logn != 12) return false;
+    if (logn != 10 && logn != 11 && logn != 12) return false;
     const int N = 1 << logn, T = N / 8;
     return g == 5 && logm == logn - 2 && a.cp == N / 4 && a.npr == 1 && a.S >= 1 && a.S <= RX_SMAX &&
            a.D >= 2 && a.D <= RX_DPT * T && a.P >= 1 && a.P <= T && cfo_p == a.P &&
-           (logn == 11 ? wide_shm<11>(a) : wide_shm<12>(a)) <= 160 * 1024;
+           (logn == 10 ? wide_shm<10>(a) : logn == 11 ? wide_shm<11>(a) : wide_shm<12>(a)) <= 160 * 1024;
 }
 
 hipError_t launch_stream_decode_wide(const CfoArgs& c, const StreamParamsArgs& a, const RxArgs& r, int logn,
                                      hipStream_t st)
 {
     if (a.nframes <= 0) return hipSuccess;
+    if (logn == 10) return r.iq16 ? wide_launch<10, true>(c, a, r, st) : wide_launch<10, false>(c, a, r, st);
     if (logn == 11) return r.iq16 ? wide_launch<11, true>(c, a, r, st) : wide_launch<11, false>(c, a, r, st);
     if (logn == 12) return r.iq16 ? wide_launch<12, true>(c, a, r, st) : wide_launch<12, false>(c, a, r, st);
     return hipErrorNotSupported;

@@ -309,6 +309,11 @@ def test_stream_wide_fused_decode_matches_oracle_and_staged(name):
 
 
 WIDE_VARIANTS = {
+    # N = 1024, cp = N/4: 1280-point CFO form of 5 x 256 (two CFO transforms
+    # per wave, a dummy one on the third wave's spare lanes)
+    "N1024": dict(B, fft_size=1024, num_data_subc=512, num_pilot_subc=16, cp_size=256),
+    "N1024_qam16_s5": dict(B, fft_size=1024, num_data_subc=512, num_pilot_subc=16, cp_size=256, mod_type=4,
+                           num_symb=5),
     "B_s3": dict(B, num_symb=3),                                   # odd S: group 1 idle in the last step
     "B_s5_qam16": dict(B, num_symb=5, mod_type=4),
     "B_d512_p16": dict(B, num_data_subc=512, num_pilot_subc=16),  # D < 4T, half = T
@@ -329,6 +334,18 @@ def test_stream_wide_fused_decode_geometry_variants(name):
     assert len(want) >= 4
     assert np.array_equal(fused[1], staged[1]) and np.array_equal(fused[2], staged[2])
     assert np.array_equal(fused[4], staged[4]) and rel_err(fused[3], staged[3]) < 1e-9
+
+
+@pytest.mark.parametrize("name,cfg", [("B_cp0", dict(B, cp_size=0)), ("D_cp0", dict(D, cp_size=0)),
+                                      ("N1024_cp0", dict(B, fft_size=1024, num_data_subc=512, num_pilot_subc=16,
+                                                         cp_size=0))])
+def test_stream_cp_not_quarter_matches_oracle(name, cfg):
+    # cp != N/4: a 2^a-point CFO form (no radix-5 combine), decoded by the
+    # staged cfo -> params -> rx kernels; every located frame against the
+    # oracle (CFO and bytes exact, constellation 1e-9, no decision flips)
+    x, data = impaired_stream(cfg, 8, seed=25)
+    want = check_against_oracle(cfg, x, run_stream(cfg, x, chunk=40000))
+    assert len(want) >= 4
 
 
 def test_stream_wide_fused_decode_i16_equals_f64():
