@@ -1572,7 +1572,7 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
                        c->npr == 1 && c->S + 1 <= 64 && c->L % (c->N / 8) == 0 && c->L / (c->N / 8) <= 16 &&
                        c->cp <= 2 * (c->N / 8) &&  // stream_params_kernel: CP template in 2 registers
                        cfo_plan(c, c->npr, &pl) == OFDM_OK;
-    const size_t per = (size_t)c->D * sizeof(double2) + (size_t)c->S * 4 * sizeof(double) + sizeof(double);
+    const size_t per = (size_t)c->D * sizeof(double2) + (size_t)c->S * ofdm::CORR_PER_SYM * sizeof(double2) + sizeof(double);
     const long npts = (long)c->D * c->S;
     // frames [0, nb) of d_list (device count d_cnt, if set, bounds them further)
     auto decode_fused = [&](const long* d_list, size_t nb_total, const long* d_cnt) -> int {
@@ -1581,8 +1581,8 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
         int r2;
         if ((r2 = grow(c, c->s_chan, nb0 * per))) return r2;
         double2* chan = static_cast<double2*>(c->s_chan.p);
-        double* corr = reinterpret_cast<double*>(chan + nb0 * c->D);
-        double* cfo_tmp = corr + nb0 * c->S * 4;
+        double2* corr = chan + nb0 * c->D;
+        double* cfo_tmp = reinterpret_cast<double*>(corr + nb0 * c->S * ofdm::CORR_PER_SYM);
         for (size_t f0 = 0; f0 < nb_total; f0 += nb0) {
             const size_t nb = std::min(nb0, nb_total - f0);
             double* cfo = cfo_out ? cfo_out + f0 : cfo_tmp;

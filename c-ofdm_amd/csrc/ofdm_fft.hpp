@@ -72,6 +72,18 @@ __device__ __forceinline__ double2 cmul_exact(double2 a, double2 b)
                         add_rn(mul_rn(a.x, b.y), mul_rn(a.y, b.x)));
 }
 
+// cp_freq_sinh's symbol phase carg(sum_j conj(x_j) x_{j+N}) over the
+// freq-shifted samples (Frame.hpp:238-263), from the sum acc over the raw
+// samples times the shift's phasor rot. The reference's sum starts at +0, so
+// an empty or all-zero one (cp = 0) has phase 0, where the signed zeros of
+// acc * rot would give atan2(+-0, -0) = +-pi.
+__device__ __forceinline__ double cp_phase(double2 acc, double2 rot)
+{
+    if (acc.x == 0.0 && acc.y == 0.0) return 0.0;
+    const double2 r = cmul_exact(acc, rot);
+    return atan2(r.y, r.x);
+}
+
 // libgcc __divdc3 (Smith's algorithm) for finite operands — what the
 // reference's std::complex<double> operator/ compiles to.
 __device__ __forceinline__ double2 cdiv_exact(double2 n, double2 d)

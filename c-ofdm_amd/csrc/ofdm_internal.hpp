@@ -41,6 +41,14 @@ struct TxArgs {
     unsigned long long sample_offset;
 };
 
+// The staged stream decode's ramp table, per frame and message symbol:
+// CORR_PER_SYM phasors {e^{iA}, e^{iB 2^j} (j < CORR_BITS), e^{iBN/8}}. A
+// thread's start phasor e^{i(A + B t)} is e^{iA} times the powers its index
+// bits select (t < 2^CORR_BITS = 512 = the largest N/8): products of table
+// entries, no sincos in the rx, whose register window leaves no room for one.
+constexpr int CORR_BITS = 9;
+constexpr int CORR_PER_SYM = CORR_BITS + 2;  // double2 entries
+
 struct RxArgs {
     DevTables tab;
     const double2* iq;          // frame f message at iq + f*frame_stride
@@ -56,15 +64,15 @@ struct RxArgs {
     const uint8_t* ref;         // nullable
     unsigned long long* bit_errors;  // nullable
     double2* ystage;            // staged variant only: nframes*S*D scratch
-    // stream mode (fused stream decode): frame f's message body starts at
+    // stream mode (staged stream decode): frame f's message body starts at
     // starts[f] + start_off, and message symbol s is multiplied by the phase
-    // ramp e^{i(A + B m)} of corr[(f*S + s)*4 ..] = {A, B, cos(B*T), sin(B*T)}
-    // (freq_shift + cp_freq_sinh + pr_phase_sinh, ofdm_sync.hip stream_params_kernel)
+    // ramp e^{i(A + B m)} (freq_shift + cp_freq_sinh + pr_phase_sinh) whose
+    // table is corr[(f*S + s)*CORR_PER_SYM ..] (ofdm_sync.hip stream_params_kernel)
     const long* starts;         // nullable
     long start_off;
     const long* count;          // nullable: frames beyond min(*count, nframes) are skipped
     int* queue;                 // nullable: {next, done} counters (zero; left zero) for dynamic frames
-    const double* corr;
+    const double2* corr;
     int S, D, P, seg, cp, k;
     long bytes_per_frame;
     double pilot_ampl;

@@ -656,12 +656,18 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 2) rx_kernel(RxArgs a)
             if (!SYNC && s + 1 < S) pf.load(a, x0 + (long)(s + 1) * L, t);
             if constexpr (SYNC) {
                 // sample m = t + T*i of the body: *= e^{i(A + B m)}, by a
-                // running product from e^{i(A + B t)} in steps of e^{i B T}
-                const double* cr = a.corr + (f * S + s) * 4;
-                const double2 w = make_double2(cr[2], cr[3]);
-                double sn, cs;
-                sincos(cr[0] + cr[1] * (double)t, &sn, &cs);
-                double2 c = make_double2(cs, sn);
+                // running product from e^{i(A + B t)} in steps of e^{i B T};
+                // e^{i(A + B t)} from the table (uniform loads), the bits of t
+                // selecting its powers (x (1, 0) is exact)
+                // (the bit tests on a per-symbol opaque copy of t: hoisted
+                // out of the loop, their lane masks filled the SGPRs and spilled)
+                const double2* rt = a.corr + (f * S + s) * CORR_PER_SYM;
+                int tr;
+                asm volatile("v_mov_b32 %0, %1" : "=v"(tr) : "v"(t));
+                double2 c = rt[0];
+#pragma unroll
+                for (int j = 0; j < LOGN - 3; ++j) c = cmul_exact(c, (tr >> j) & 1 ? rt[1 + j] : make_double2(1.0, 0.0));
+                const double2 w = rt[CORR_PER_SYM - 1];
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
                     v[i] = cmul(v[i], c);
@@ -1055,7 +1061,7 @@ __global__ void __launch_bounds__(128, 3) rx_stream2_kernel(RxArgs a)
         const double2* chan = a.chan + f * a.chan_stride;
         for (int d = tid; d < D; d += 128) L.chl[d] = chan[d];
         __syncthreads();  // twiddles (first frame) and the channel visible
-        rx2_frame<I16>(a, f, L, a.corr + f * S * 4, pk, pbin);
+        rx2_frame<I16>(a, f, L, reinterpret_cast<const double*>(a.corr + f * S * CORR_PER_SYM), pk, pbin);
     }
 }
 

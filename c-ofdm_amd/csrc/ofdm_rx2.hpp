@@ -53,8 +53,8 @@ struct Rx2Lds {
 constexpr int RT_PER_SYM = 12;
 __host__ __device__ constexpr int rt_size(int S) { return RT_PER_SYM * S + 3; }  // double2 entries
 
-// Frame f of a.starts (message body at starts[f] + start_off); corr: its S*4
-// ramp numbers {A, B, cos(B*T), sin(B*T)} (global or LDS), or (TAB) the
+// Frame f of a.starts (message body at starts[f] + start_off); corr: its S
+// ramp tables of CORR_PER_SYM phasors (ofdm_internal.hpp), or (TAB) the
 // table above, from which the channel reciprocals are made too; chan_g: nullptr,
 // or the frame's D channel reciprocals in global memory, requested after the
 // transforms and stored to L.chl after the gains (loads issued among the
@@ -112,11 +112,12 @@ __device__ __forceinline__ void rx2_frame(const RxArgs& a, long f, const Rx2Lds&
                 }
                 wr = rt[11];
             } else {
-                const double* cr = corr + s * 4;
-                double sn, cs;
-                sincos(cr[0] + cr[1] * (double)lq, &sn, &cs);
-                c = make_double2(cs, sn);
-                wr = make_double2(cr[2], cr[3]);
+                // the staged decode's table (CORR_PER_SYM per symbol)
+                const double2* rt = reinterpret_cast<const double2*>(corr) + s * CORR_PER_SYM;
+                c = rt[0];
+#pragma unroll
+                for (int j = 0; j < 6; ++j) c = cmul_exact(c, (lq >> j) & 1 ? rt[1 + j] : make_double2(1.0, 0.0));
+                wr = rt[CORR_PER_SYM - 1];
             }
             asm volatile("" ::: "memory");
             double2 v[8];

@@ -284,8 +284,7 @@ __global__ void __launch_bounds__(WideGeo<LOGN>::NT, 4) stream_decode_wide_kerne
         sincospi(-2.0 * cfo * (double)N, &rs, &rc);
         if (tid < Q) {
             const double2 acc = cadd(make_double2(0.0, 0.0), cps[tid]);
-            const double2 rr = cmul_exact(acc, make_double2(rc, rs));
-            phi[tid] = atan2(rr.y, rr.x);
+            phi[tid] = cp_phase(acc, make_double2(rc, rs));
         }
     }
     __syncthreads();  // phases visible

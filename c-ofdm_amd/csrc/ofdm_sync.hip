@@ -1013,8 +1013,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 3) stream_params_kernel(Strea
     for (int q = t; q < Q; q += T) {
         double2 acc = make_double2(0.0, 0.0);
         for (int u = 0; u < NWV; ++u) acc = cadd(acc, part[q * NWV + u]);
-        const double2 r = cmul_exact(acc, make_double2(rc, rs));
-        phi[q] = atan2(r.y, r.x);
+        phi[q] = cp_phase(acc, make_double2(rc, rs));
     }
     __syncthreads();
     if (t == 0) {
@@ -1124,18 +1123,17 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 3) stream_params_kernel(Strea
         // constell /= chan would round it) instead of a division per point
         chan[i] = a.chan_recip ? cdiv_exact(make_double2(1.0, 0.0), make_double2(cs, sn)) : make_double2(cs, sn);
     }
-    // message symbols: theta(m) = A_s + B_s m over the CP-stripped body
-    for (int s = t; s < a.S; s += T) {
-        const int q = 1 + s;
-        const double A = -2.0 * M_PI * cfo * (double)((long)q * L + a.cp) - (psi[q] * L + phi[q] * a.cp) / N - phr;
+    // message symbols: theta(m) = A_s + B_s m over the CP-stripped body, as
+    // the ramp table {e^{iA}, e^{iB 2^j} (j < CORR_BITS), e^{iBT}}; B 2^j and
+    // B T are exact products (powers of two)
+    for (int e = t; e < a.S * CORR_PER_SYM; e += T) {
+        const int s = e / CORR_PER_SYM, j = e % CORR_PER_SYM, q = 1 + s;
         const double B = -2.0 * M_PI * cfo - phi[q] / N;
+        const double th = j == 0 ? -2.0 * M_PI * cfo * (double)((long)q * L + a.cp) - (psi[q] * L + phi[q] * a.cp) / N - phr
+                                 : B * (double)(j <= CORR_BITS ? 1 << (j - 1) : T);
         double sn, cs;
-        sincos(B * T, &sn, &cs);
-        double* o = a.corr_out + (f * a.S + s) * 4;
-        o[0] = A;
-        o[1] = B;
-        o[2] = cs;
-        o[3] = sn;
+        sincos(th, &sn, &cs);
+        a.corr_out[(f * a.S + s) * CORR_PER_SYM + j] = make_double2(cs, sn);
     }
 }
 
@@ -1419,8 +1417,7 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
                 acc.y += __shfl_xor(acc.y, o);
             }
             acc = cadd(make_double2(0.0, 0.0), acc);
-            const double2 rr = cmul_exact(acc, make_double2(rc, rs));
-            if (t == 0) phi[0] = atan2(rr.y, rr.x);
+            if (t == 0) phi[0] = cp_phase(acc, make_double2(rc, rs));
         }
         wave_lds_sync();
         const double slope0 = -2.0 * M_PI * cfo - phi[0] / N;
@@ -1568,8 +1565,7 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
         if (t < a.S) {
             const int q = 1 + t;
             const double2 acc = cadd(make_double2(0.0, 0.0), cps[q]);
-            const double2 r = cmul_exact(acc, make_double2(rc, rs));
-            phi[q] = atan2(r.y, r.x);
+            phi[q] = cp_phase(acc, make_double2(rc, rs));
         }
     }
     __syncthreads();  // cfo, phi[0..S], phr and the LS fit visible

@@ -199,7 +199,7 @@ struct StreamParamsArgs {
     const double2* mod_pre;     // D*npr BPSK points
     double2* chan_out;          // nframes * D
     bool chan_recip;            // write 1/chan (for rx's chan_recip mode) instead of chan
-    double* corr_out;           // nframes * S * 4: A_s, B_s, cos(B_s*T), sin(B_s*T)
+    double2* corr_out;          // nframes * S * CORR_PER_SYM: the ramp tables (ofdm_internal.hpp)
     int npr, S, D, P, cp;
     double pilot_ampl;
     const long* count;          // nullable: frames beyond min(*count, nframes) are skipped
