@@ -12,6 +12,8 @@ for order in first last; do
 import json; d=json.load(open('gpurun_out/ramp_$order.json'))
 s=d['step_ms']
 print('$order', round(d['value']/1e9,2), 'G; step ms in groups of 10:', [round(sum(s[i:i+10])/10,4) for i in range(0,len(s),10)])
-print('   first 12:', s[:12])" >> $OUT
+print('   first 12:', s[:12])
+c=d.get('config3')
+if c: print('   config3 step ms:', c['step_ms'])" >> $OUT
 done
 cat $OUT
