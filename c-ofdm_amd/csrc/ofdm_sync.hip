@@ -2296,6 +2296,7 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
         prof[1] = 0;
         prof[3] = 0;
         prof[4] = 0;
+        for (int i = 8; i < WALK_PROF_FIELDS; ++i) prof[i] = 0;
     }
     long pos = a.start_pos ? a.start_pos[blockIdx.x] : (c == 0 ? a.start : (core0 > a.halo ? core0 - a.halo : 0));
     const bool ring = a.ring > 0;  // uniform
@@ -2353,6 +2354,7 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
         // find_t2sin(pos): blocks pos + k*N, first hit wins
         long hit = -1;
         bool stop = false;
+        const long prof_t2 = PROF ? (long)wall_clock64() : 0;
         // FP64: G blocks from `base` (block g per group of T threads); the
         // first block whose ratio exceeds the level (Frame.hpp:150-197), or
         // INT_MAX. Slot sl collects the first hit; slot sl + 1 (mod 3) is reset
@@ -2406,6 +2408,7 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
                     sine += red[g * NW + w].y;
                 }
             }
+            if (long* prof = WALK_PROF; prof && t == 0) ++prof[11];
             int* hslot = bslot + sl;
             const int nx = sl == 2 ? 0 : sl + 1;
             if (t == 0) {  // both slots of the next evaluation, whichever kind it is
@@ -2462,6 +2465,7 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
                     }
                     int tt;  // opaque per-step copy (see t2_eval64)
                     asm volatile("v_mov_b32 %0, %1" : "=v"(tt) : "v"(tt0));
+                    if (long* prof = WALK_PROF; prof && t == 0) ++prof[10];
                     const long bA = base + (long)g * N, bB = bA + (long)G * N;
                     const bool liveA = ring ? (bA + N <= rend && bA < a.n) : bA + N <= a.n;
                     const bool liveB = ring ? (bB + N <= rend && bB < a.n) : bB + N <= a.n;
@@ -2554,6 +2558,7 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
                     miss = ss == 2;
                     break;
                 }
+                if (long* prof = WALK_PROF; prof && t == 0) ++prof[10];
                 const int bg = t2_eval64(base);
                 if (bg != INT_MAX) {
                     hit = base + (long)bg * N;
@@ -2561,6 +2566,7 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
                 }
             }
         }
+        if (long* prof = WALK_PROF; prof && t == 0) prof[8] += (long)wall_clock64() - prof_t2;
         if (stop) break;
         if (miss) {  // rx.cpp:137-145: pos = output_size of the next buffer
             pos = rend;
@@ -2568,10 +2574,15 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
             continue;
         }
         if (ring && hit >= rend - a.out_len) rend += a.ring;  // rx.cpp:147-156: carry, next buffer
+        const long prof_pre = PROF ? (long)wall_clock64() : 0;
         const int lag = (a.tspec && !a.exact_only)
                             ? walk_preamble_fft<WT, F>(a, hit, big, P, tw_m, reinterpret_cast<int*>(scr + 2), xs, normv,
                                                     best, t)
                             : walk_preamble<WT, F>(a, hit, xs, ctap, E, normv, best, unsure, mred, t);
+        if (long* prof = WALK_PROF; prof && t == 0) {
+            prof[9] += (long)wall_clock64() - prof_pre;
+            ++prof[12];
+        }
         // rx.cpp:160-168: find_preamble's -10 (no lag passes) moves on by a
         // message. rx.cpp tests preamble_begin < -2 in buffer coordinates,
         // where a found preamble gives >= 1; in stream coordinates a found
@@ -2590,10 +2601,16 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
         const long rv = (ring && pb >= 0 && rend != ring_after(pb + a.msg)) ? (pb | WALK_REC_LAG) : pb;
         if (t == 0 && nrec < a.max_rec) {
             long* rp = a.rec + (long)c * a.max_rec + nrec;
-            if (lb) {  // published for the walkers that look back on this chunk
+            if (lb) {
+                // published for the walkers that look back on this chunk: the
+                // count of the previous record goes out now (its store landed
+                // long ago: the wait is free), this record's with the next one,
+                // before any look-back wait of this walker, or at the end
+                if (nrec > 0) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __hip_atomic_store(a.pub + c, nrec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
                 __hip_atomic_store(rp, rv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __hip_atomic_store(a.pub + c, nrec + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
                 *rp = rv;
             }
@@ -2612,7 +2629,12 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
                 break;
             }
             int* lbres = reinterpret_cast<int*>(scr + 8);
-            if (t == 0) *lbres = lookback_find(a, pb, rv, WALK_PROF);
+            if (t == 0) {
+                // every record of this walk published before it waits on another
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(a.pub + c, nrec + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                *lbres = lookback_find(a, pb, rv, WALK_PROF);
+            }
             __syncthreads();
             const int j = *lbres;
             if (j >= 0) {  // this walk joins chunk m's from this frame on: done

@@ -152,10 +152,12 @@ struct WalkArgs {
     int* link;
     // nullable diagnostics (OFDM_WALK_PROF): per chunk {start, core end,
     // end (wall_clock64 ticks), frames past the core end, look-back polls
-    // that waited, workgroup, XCC id, frames located}
+    // that waited, workgroup, XCC id, frames located, ticks in the T2 scans,
+    // ticks in the preamble searches, scan steps, FP64 T2 evaluations,
+    // preamble searches}
     long* prof;
 };
-constexpr int WALK_PROF_FIELDS = 8;
+constexpr int WALK_PROF_FIELDS = 13;
 constexpr int WALK_PUB_DONE = 1 << 30;
 // a walker waits at most this many polls for the chunk it looks back on
 constexpr int WALK_SPIN_MAX = 1 << 16;

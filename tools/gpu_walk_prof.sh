@@ -1,9 +1,9 @@
 #!/bin/bash
 # walker timelines (OFDM_WALK_PROF) of stream_bench.py calls, f64 / int16,
-# look-back with 1 and 2 chunks per slot and the halo walk
+# look-back with 1 and 2 chunks per slot and the halo walk (TUNINGS=... to pick)
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-for tun in "chunks_per_slot=1" "chunks_per_slot=2" "lookback=0"; do
+for tun in ${TUNINGS:-chunks_per_slot=1 chunks_per_slot=2 lookback=0}; do
   for args in "--frames 16384" "--frames 16384 --i16"; do
     tag=$(echo "$tun$args" | tr -c 'a-z0-9' '_')
     rm -f gpurun_out/wp_$tag.jsonl
@@ -12,6 +12,7 @@ for tun in "chunks_per_slot=1" "chunks_per_slot=2" "lookback=0"; do
     python3 -c "
 import json,sys; d=json.load(open('gpurun_out/wp_$tag.summary.json'))['calls'][-1]
 print('$tun $args', 'span', d['kernel_span_us'], 'walker pct', d['walker_us_pct_0_10_50_90_99_100'], 'mean', d['walker_mean_us'], 'start pct', d['start_us_pct'], 'ext', d['ext_frames_hist'], 'waits', d['waits_total'], d['chunks_that_waited'])
+print('   phases', d.get('phases'))
 print('   tail', [(t['chunk'], t['start_us'], t['end_us'], t['core_us'], t['ext_frames'], t['waits'], t['nrec']) for t in d['tail_chunks'][:5]])
 "
   done

@@ -17,7 +17,7 @@ TICK_US = 0.01  # wall_clock64: 100 MHz
 
 def summarise(d):
     a = np.array(d["chunks"], dtype=np.int64)
-    t0, tc, te, ext, waits, blk, xcc, nrec = a.T
+    t0, tc, te, ext, waits, blk, xcc, nrec = a.T[:8]
     base = t0.min()
     start, end = (t0 - base) * TICK_US, (te - base) * TICK_US
     dur = end - start
@@ -25,7 +25,7 @@ def summarise(d):
     span = end.max()
     late = np.argsort(end)[-8:][::-1]
     q = lambda v: [round(float(x), 1) for x in np.percentile(v, [0, 10, 50, 90, 99, 100])]
-    return {
+    out = {
         "nchunks": d["nchunks"], "chunk": d["chunk"], "lookback": d["lookback"], "grid": d["grid"],
         "kernel_span_us": round(float(span), 1),
         "walker_us_pct_0_10_50_90_99_100": q(dur), "walker_mean_us": round(float(dur.mean()), 1),
@@ -38,6 +38,20 @@ def summarise(d):
                          "nrec": int(nrec[c]), "xcc": int(xcc[c]), "block": int(blk[c])} for c in late],
         "end_by_xcc_max_us": {int(x): round(float(end[xcc == x].max()), 1) for x in np.unique(xcc)},
     }
+    if a.shape[1] >= 13:  # phase split: T2 scans, preamble searches (ticks), scan steps, FP64 evaluations, searches
+        t2, pre, steps, f64, nsearch = a.T[8:13]
+        nf = max(int(nsearch.sum()), 1)
+        out["phases"] = {
+            "t2_scan_us_per_walker": round(float(t2.mean()) * TICK_US, 1),
+            "preamble_us_per_walker": round(float(pre.mean()) * TICK_US, 1),
+            "other_us_per_walker": round(float(dur.mean() - (t2.mean() + pre.mean()) * TICK_US), 1),
+            "t2_scan_us_per_search": round(float(t2.sum()) * TICK_US / nf, 2),
+            "preamble_us_per_search": round(float(pre.sum()) * TICK_US / nf, 2),
+            "scan_steps_per_search": round(float(steps.sum()) / nf, 2),
+            "fp64_evals_per_search": round(float(f64.sum()) / nf, 3),
+            "searches_per_walker": round(float(nsearch.mean()), 2),
+        }
+    return out
 
 
 def main():
