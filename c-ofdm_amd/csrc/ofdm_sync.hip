@@ -2154,10 +2154,11 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
 // with record r at pb, past its own core end and inside chunk m's core: the
 // index of r in m's published records, or -1 when m's walk does not hold it
 // (m published a record past pb, or finished). While m has not reached pb
-// the walker waits for it, but only once m has been taken from the queue: its
-// walker is then resident (the grid is at most the resident walker count),
-// and it publishes every record before any wait of its own, so the wait
-// ends. Records and counts are stored write-through
+// the walker waits for it, but only once m's walker has started (it marks its
+// chunk WALK_PUB_STARTED: running, not merely queued or waiting for a CU
+// behind another kernel's workgroups), and that walker publishes every
+// record before any wait of its own, so the wait ends. Records and counts are
+// stored write-through
 // (sc1) by the publishing lane, which drains its stores before each count;
 // every load here is an sc1 load of them.
 __device__ int lookback_find(const WalkArgs& a, long pb, long r, long* prof)
@@ -2167,18 +2168,15 @@ __device__ int lookback_find(const WalkArgs& a, long pb, long r, long* prof)
     for (int spin = 0;; ++spin) {
         const int pv = __hip_atomic_load(a.pub + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // the record loads stay behind the poll
-        const int cnt = min(pv & (WALK_PUB_DONE - 1), a.max_rec);
+        const int cnt = min(pv & WALK_PUB_COUNT, a.max_rec);
         for (int j = 0; j < cnt; ++j) {
             const long v = __hip_atomic_load(rm + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (v == r) return j;
             if ((v < 0 ? v : (v & WALK_REC_PB)) > pb) return -1;  // m's walk passed pb without this frame
         }
         if (pv & WALK_PUB_DONE) return -1;
-        // taken: a first-round chunk (m < grid: every workgroup of the grid
-        // is resident), or one the queue has handed out
-        if (spin >= WALK_SPIN_MAX ||
-            (m >= gridDim.x && __hip_atomic_load(a.queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + (long)gridDim.x <= m))
-            return -1;  // m not taken yet: walk on (always exact), and look again at the next frame
+        if (spin >= WALK_SPIN_MAX || !(pv & WALK_PUB_STARTED))
+            return -1;  // m's walker not running: walk on (always exact), and look again at the next frame
         if (prof) ++prof[4];
         __builtin_amdgcn_s_sleep(4);
     }
@@ -2288,7 +2286,10 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
     const long end = lb ? a.core_hi : cend;
     // look-back link {chunk this walk joins, the shared frame's index here and
     // there}: none until the walk joins one
-    if (lb && t0 == 0) a.link[3 * c] = -1;
+    if (lb && t0 == 0) {
+        a.link[3 * c] = -1;
+        __hip_atomic_store(a.pub + c, WALK_PUB_STARTED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     // diagnostics (a.prof): stored as they happen, nothing held in registers
 #define WALK_PROF (PROF ? a.prof + (long)c * WALK_PROF_FIELDS : nullptr)
     if (long* prof = WALK_PROF; prof && t0 == 0) {
@@ -2608,7 +2609,7 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
                 // before any look-back wait of this walker, or at the end
                 if (nrec > 0) {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    __hip_atomic_store(a.pub + c, nrec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(a.pub + c, nrec | WALK_PUB_STARTED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
                 __hip_atomic_store(rp, rv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
@@ -2632,7 +2633,8 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
             if (t == 0) {
                 // every record of this walk published before it waits on another
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __hip_atomic_store(a.pub + c, nrec + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(a.pub + c, (nrec + 1) | WALK_PUB_STARTED, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
                 *lbres = lookback_find(a, pb, rv, WALK_PROF);
             }
             __syncthreads();

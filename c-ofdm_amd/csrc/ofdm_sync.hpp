@@ -159,6 +159,10 @@ struct WalkArgs {
 };
 constexpr int WALK_PROF_FIELDS = 13;
 constexpr int WALK_PUB_DONE = 1 << 30;
+// set by a chunk's walker when it starts (with the count, until DONE): a
+// walker looks back on (waits for) only a chunk whose walker is running
+constexpr int WALK_PUB_STARTED = 1 << 29;
+constexpr int WALK_PUB_COUNT = WALK_PUB_STARTED - 1;
 // a walker waits at most this many polls for the chunk it looks back on
 constexpr int WALK_SPIN_MAX = 1 << 16;
 // A walk record is a preamble start, plus in ring mode the walk state after
