@@ -26,17 +26,19 @@ def main():
     cons = torch.empty((nf * p["num_data_subc"] * 8,), dtype=torch.complex128, device="cuda")
     out = torch.empty_like(data)
     errs = torch.zeros((1,), dtype=torch.int64, device="cuda")
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-    times = []
-    for _ in range(30):
-        ev[0].record()
+    steps = int(os.environ.get("AB_STEPS", "60"))
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    # back to back, as bench.py times them (no host sync between steps: the
+    # clocks stay up); the first third is warmup
+    for e in ev:
+        e[0].record()
         m.tx(data, nf, iq, noise_std=0.447, seed=1)
-        ev[1].record()
+        e[1].record()
         m.rx(iq, nf, constell_out=cons, bytes_out=out, ref=data, bit_errors=errs)
-        ev[2].record()
-        torch.cuda.synchronize()
-        times.append((ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])))
-    t = np.array(times[10:])
+        e[2].record()
+    torch.cuda.synchronize()
+    times = [(e[0].elapsed_time(e[1]), e[1].elapsed_time(e[2])) for e in ev]
+    t = np.array(times[steps // 3:])
     print(json.dumps({"lib": os.path.basename(os.environ.get("OFDM_MI355X_LIB", "product")),
                       "tx_ms": float(np.median(t[:, 0])), "rx_ms": float(np.median(t[:, 1])),
                       "rx_min_ms": float(t[:, 1].min()), "step_ms": float(np.median(t.sum(1)))}), flush=True)
