@@ -596,18 +596,26 @@ def main():
 
     deferred = []
     sub = {}
-    if not args.no_stream:
-        sub["stream"] = stream_leg(args, dist, dev, world, rank, M, i16=False, deferred=deferred)
-        sub["stream_int16"] = stream_leg(args, dist, dev, world, rank, M, i16=True, deferred=deferred)
-        if args.stream_b_frames > 0:  # the wide-geometry fused decode (config B frames) against the staged kernels
-            torch.cuda.empty_cache()
-            sub["stream_B"] = stream_leg(args, dist, dev, world, rank, M, i16=False, p=CONFIG_B,
-                                         frames_per_gpu=args.stream_b_frames, workload=STREAM_WORKLOAD_B,
-                                         pipeline=False, staged_ab=True, deferred=deferred)
-    if not args.no_config3:
+
+    def record(name, fn):
+        # a sub-record that raises is reported in its field, and the headline
+        # is still measured (every rank runs the same legs, so a failure that
+        # comes from the configuration fails on all of them alike)
+        try:
+            sub[name] = fn()
+        except Exception as e:
+            sub[name] = {"error": repr(e)}
+            print(f"bench.py: sub-record {name} failed: {e!r}", file=sys.stderr)
         torch.cuda.empty_cache()
-        sub["config3"] = config3_leg(args, dist, dev, world, rank, M)
-    torch.cuda.empty_cache()
+    if not args.no_stream:
+        record("stream", lambda: stream_leg(args, dist, dev, world, rank, M, i16=False, deferred=deferred))
+        record("stream_int16", lambda: stream_leg(args, dist, dev, world, rank, M, i16=True, deferred=deferred))
+        if args.stream_b_frames > 0:  # the wide-geometry fused decode (config B frames) against the staged kernels
+            record("stream_B", lambda: stream_leg(args, dist, dev, world, rank, M, i16=False, p=CONFIG_B,
+                                                  frames_per_gpu=args.stream_b_frames, workload=STREAM_WORKLOAD_B,
+                                                  pipeline=False, staged_ab=True, deferred=deferred))
+    if not args.no_config3:
+        record("config3", lambda: config3_leg(args, dist, dev, world, rank, M))
 
     def step(i, events=None):
         if events:

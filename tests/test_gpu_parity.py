@@ -324,7 +324,10 @@ def test_full_size_loopback_config_b():
     # the GPU noise equals the oracle's counter-based noise
     clean = O.tx_batch(B, data[: g["bytes_per_frame"]], 1)
     noisy = O.awgn(clean, float(np.sqrt(2.0 / 10.0)), seed=11)
-    assert rel_err(h[0], noisy) < 1e-5  # FP32 transcendental noise (channel model) vs FP64 oracle
+    # the channel model's tolerance, on the noise component: the GPU's FP32
+    # Box-Muller transcendentals against the oracle's FP64 draw of the same
+    # counters (measured ~1e-7)
+    assert rel_err(h[0] - clean, noisy - clean) < 1e-6
 
 
 def test_awgn_counter_crosses_2_32_boundary():
@@ -342,7 +345,7 @@ def test_awgn_counter_crosses_2_32_boundary():
     clean = O.tx_batch(B, data, nf)
     want = O.awgn(clean, 0.3, seed=seed, sample_offset=off)
     got = host(iq)
-    assert rel_err(got - clean, want - clean) < 1e-5  # FP32 transcendentals vs FP64 oracle
+    assert rel_err(got - clean, want - clean) < 1e-6  # the channel model's tolerance on the noise
 
 
 def test_full_size_config_c_roundtrip():
@@ -445,8 +448,9 @@ def test_config3_ber_sweep_points_match_oracle():
     h = host(iq)
     _, ob, _ = O.rx_batch(CC, h, nf, g["message_len"])
     assert np.array_equal(ob, host(out))
-    want = O.awgn(O.tx_batch(CC, data, nf), std, seed=1010)
-    assert rel_err(h, want) < 1e-5  # FP32 transcendentals in the GPU channel
+    clean = O.tx_batch(CC, data, nf)
+    want = O.awgn(clean, std, seed=1010)
+    assert rel_err(h - clean, want - clean) < 1e-6  # the channel model's tolerance on the noise
 
 
 def test_full_size_config_b_every_frame_matches_oracle():
