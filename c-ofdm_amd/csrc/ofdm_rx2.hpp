@@ -88,6 +88,17 @@ __device__ __forceinline__ void rx2_frame(const RxArgs& a, long f, const Rx2Lds&
     double2* img = L.img + w * N;
     const long x0 = a.starts[f] + a.start_off;
     double2 y[SH][RX_DPT];
+    // complex<int16> input: the wave's next symbol is requested before this
+    // one's transform (8 registers), so its HBM latency hides behind it
+    int rnext[8];
+    auto load16 = [&](int s, int l) {
+        const int* p = reinterpret_cast<const int*>(a.iq16 + x0 + (long)s * Lf + l);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) rnext[i] = __builtin_nontemporal_load(p + T * i);
+    };
+    if constexpr (I16) {
+        if (w < S) load16(w, lane);
+    }
     // the wave's symbols, unrolled (compile-time window registers); each
     // starts from an opaque lane copy and a memory fence, so nothing of one
     // symbol (loads, LDS addresses) is hoisted and held across another
@@ -123,13 +134,11 @@ __device__ __forceinline__ void rx2_frame(const RxArgs& a, long f, const Rx2Lds&
             double2 v[8];
             const long off = x0 + (long)s * Lf + lq;
             if constexpr (I16) {
-                const int* p = reinterpret_cast<const int*>(a.iq16 + off);
-                int r[8];
-#pragma unroll
-                for (int i = 0; i < 8; ++i) r[i] = __builtin_nontemporal_load(p + T * i);
+                (void)off;
 #pragma unroll
                 for (int i = 0; i < 8; ++i)
-                    v[i] = make_double2((double)(int)(short)(r[i] & 0xffff), (double)(r[i] >> 16));
+                    v[i] = make_double2((double)(int)(short)(rnext[i] & 0xffff), (double)(rnext[i] >> 16));
+                if (s + 2 < S) load16(s + 2, lq);  // uniform
             } else {
 #pragma unroll
                 for (int i = 0; i < 8; ++i) v[i] = load_nt(a.iq + off + T * i);
