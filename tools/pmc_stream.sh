@@ -16,7 +16,7 @@ for ctr, path in (("FETCH_SIZE", f"gpurun_out/pmcs_fetch{suf}/run_counter_collec
                   ("WRITE_SIZE", f"gpurun_out/pmcs_write{suf}/run_counter_collection.csv")):
     for r in csv.DictReader(open(path)):
         k = r["Kernel_Name"]
-        for key in ("stream_walk_kernel", "stream_decode_wide_kernel", "compact_kernel", "cfo_kernel", "stream_params_kernel", "stream_sync_kernel",
+        for key in ("stream_walk_kernel", "stream_decode_wide_kernel", "compact_kernel", "resolve_kernel", "cfo_kernel", "stream_params_kernel", "stream_sync_kernel",
                     "rx_stream2_kernel", "stream_decode_kernel", "rx_kernel"):
             if key in k and r["Counter_Name"] == ctr:
                 acc[(key, ctr)].append(float(r["Counter_Value"]))
