@@ -473,7 +473,7 @@ def config3_leg(args, dist, dev, world, rank, M):
         ofdm_dist.reduce_counters(cnt, dist)
         e, b = (int(v) for v in cnt.cpu().numpy())
         rows.append({"es_n0_db": db, "bits": b, "bit_errors": e, "ber": e / b})
-    for _ in range(args.warmup):
+    for _ in range(args.config3_warmup):
         step()
     torch.cuda.synchronize(dev)
     if dist:
@@ -493,7 +493,8 @@ def config3_leg(args, dist, dev, world, rank, M):
     return {"metric": "IQ-samples/sec (tx IFFT+CP and rx FFT+equalise), config C 4096-subcarrier 16-QAM frames",
             "workload": f"config3_C_N4096_D2048_P64_cp1024_16QAM_{nf}frames_x8sym_per_gpu",
             "value": world * args.steps * nf * msg / elapsed, "unit": "IQ-samples/s", "n_gpus": world,
-            "scaling": "weak", "steps": args.steps, "ms_per_step": elapsed / args.steps * 1e3, "dtype": "f64",
+            "scaling": "weak", "steps": args.steps, "warmup": args.config3_warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "dtype": "f64",
             "tx_avg_launch_ms": tx_ms, "rx_avg_launch_ms": rx_ms,
             "step_ms": [round(e[0].elapsed_time(e[2]), 4) for e in ev],
             "roofline": {"bound": "hbm", "kernel": "rx (CP strip+FFT+equalise+demap), config C",
@@ -523,7 +524,8 @@ def main():
     ap.add_argument("--no-stream", action="store_true", help="skip the config-4 stream sub-record")
     ap.add_argument("--stream-frames", type=int, default=16384, help="config-4 stream frames per GPU (weak)")
     ap.add_argument("--stream-reps", type=int, default=10)
-    ap.add_argument("--stream-warmup", type=int, default=10, help="untimed stream calls (clocks ramp)")
+    ap.add_argument("--stream-warmup", type=int, default=40,
+                    help="untimed stream calls (the clocks ramp over ~30 ms of load; the stream legs run first)")
     ap.add_argument("--stream-cpu-budget", type=float, default=8.0)
     ap.add_argument("--stream-b-frames", type=int, default=4096,
                     help="config-B stream frames per GPU for the stream_B sub-record (0: skip)")
@@ -531,6 +533,7 @@ def main():
                     help="contexts for the stream record's pipelined figure (1: off; one GPU only)")
     ap.add_argument("--no-config3", action="store_true", help="skip the config-3 (config C) sub-record")
     ap.add_argument("--config3-frames", type=int, default=4096, help="config C frames per GPU (weak)")
+    ap.add_argument("--config3-warmup", type=int, default=30, help="untimed config-3 steps (clock ramp)")
     ap.add_argument("--check-frames", default="",
                     help="comma-separated GLOBAL frame indices: after the timed steps each rank holding one writes "
                          "its noisy IQ, decoded bytes and constellation to --check-out (parity tests)")
