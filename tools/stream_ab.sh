@@ -20,13 +20,13 @@ import csv, json, sys
 lib, mode, stats, log = sys.argv[1:5]
 k = {}
 for x in csv.DictReader(open(stats)):
-    for key in ("stream_walk_kernel", "compact_kernel", "stream_decode_kernel"):
+    for key in ("stream_walk_kernel", "compact_kernel", "resolve_kernel", "stream_decode_kernel"):
         if key in x["Name"]:
             k[key] = round(float(x["AverageNs"]) / 1000, 1)
 line = [l for l in open(log) if l.startswith("{")][-1]
 d = json.loads(line)
 print(f"{lib:28s} {mode or 'f64':6s} walk {k.get('stream_walk_kernel')} compact {k.get('compact_kernel')} "
-      f"decode {k.get('stream_decode_kernel')} us | call {d['ms']} ms {d['G_stream_samples_per_s']} G")
+      f"resolve {k.get('resolve_kernel')} decode {k.get('stream_decode_kernel')} us | call {d['ms']} ms {d['G_stream_samples_per_s']} G")
 PY
     done
   done
