@@ -273,6 +273,39 @@ def test_stream_calls_on_alternating_streams_one_context():
         assert np.array_equal(host(cfo)[:k], ref[4])
 
 
+def test_stream_two_contexts_concurrent_lookback_walks():
+    # two contexts receiving on two HIP streams in turn, no host sync between
+    # calls: one call's look-back walk runs beside the other context's decode,
+    # so walkers of a grid are not all resident at once; a walker waits only on
+    # chunks whose walker has started (WALK_PUB_STARTED), and every call's
+    # outputs equal the serial call's
+    x, _ = impaired_stream(D, 1200, seed=13)
+    mf = 1536
+    for chunk in (0, 6000):
+        ref = run_stream(D, x, max_frames=mf, chunk=chunk)
+        mods = [modem(D), M.Modem(D, 0)]
+        g = O.geometry(D)
+        dx = dev(x)
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        bufs = [(torch.full((mf,), -1, dtype=torch.int64, device="cuda"),
+                 torch.zeros((mf * g["bytes_per_frame"],), dtype=torch.uint8, device="cuda"),
+                 torch.zeros((mf * g["npts"],), dtype=torch.complex128, device="cuda")) for _ in range(6)]
+        torch.cuda.synchronize()
+        outs = []
+        for k, (pbs, out, cons) in enumerate(bufs):
+            nf = mods[k % 2].rx_stream(dx, len(x), mf, pb_out=pbs, bytes_out=out, constell_out=cons, chunk=chunk,
+                                       stream=streams[k % 2])
+            outs.append((nf, pbs, out, cons))
+        torch.cuda.synchronize()
+        mods[1].close()
+        for nf, pbs, out, cons in outs:
+            k = min(nf, mf)
+            assert nf == ref[0]
+            assert np.array_equal(host(pbs)[:k], ref[1])
+            assert np.array_equal(host(out).reshape(mf, -1)[:k], ref[2])
+            assert np.array_equal(host(cons).reshape(mf, -1)[:k], ref[3])
+
+
 def test_stream_unfused_decode_path():
     # num_symb = 12 exceeds the rx register window, so the located frames take
     # the gather + staged sync chain + staged rx path instead of the fused decode
