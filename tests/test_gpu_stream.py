@@ -473,6 +473,26 @@ def test_stream_i16_synthetic_equals_f64_path():
     check_against_oracle(D, xd, ref)
 
 
+@pytest.mark.parametrize("name,cfg", [
+    ("N1024", WIDE_VARIANTS["N1024"]),                    # the wide fused decode, N = 1024
+    ("B_cp0", dict(B, cp_size=0)),                        # staged decode (ramp table), N = 2048
+    ("D_cp0", dict(D, cp_size=0)),                        # staged decode, N = 512 (rx_stream2)
+])
+def test_stream_i16_equals_f64_path_other_geometries(name, cfg):
+    # complex<int16> wire input through the decode kernels of the other
+    # geometries (each instantiated per stream format): bit-identical to the
+    # f64 path on the converted samples, which matches the oracle
+    x, _ = impaired_stream(cfg, 8, seed=29)
+    x16 = to_i16(x * 200.0)
+    xd = x16[0::2].astype(np.float64) + 1j * x16[1::2].astype(np.float64)
+    got = run_stream_i16(cfg, x16, chunk=40000)
+    ref = run_stream(cfg, xd, chunk=40000)
+    assert got[0] == ref[0] and got[0] >= 4
+    for a, b in zip(got[1:], ref[1:4]):
+        assert np.array_equal(a, b)
+    check_against_oracle(cfg, xd, ref)
+
+
 @pytest.mark.parametrize("name,cfg", [("B", B), ("D", D)])
 def test_rx_i16_equals_rx_on_converted_samples(name, cfg):
     m = modem(cfg)
