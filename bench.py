@@ -217,7 +217,7 @@ def stream_leg(args, dist, dev, world, rank, M, i16: bool, p=None, frames_per_gp
             "cfo_out": torch.zeros((cap,), dtype=torch.float64, device=dev)}
     stream = torch.cuda.current_stream(dev)
     walk = SS.hip_walker(modem, x, nsl, rx.own_lo - rx.slice_lo, rx.own_hi - rx.slice_lo, cap, outs, i16=i16,
-                         stream=stream)
+                         stream=stream, report_cap=rx.cap)
     exchange0 = SS.torch_exchange(dist, ofdm_dist.collective_device(dist, dev))
     xt = [0.0]  # host seconds inside the report all-gathers (the one collective of a call)
 
@@ -259,6 +259,20 @@ def stream_leg(args, dist, dev, world, rank, M, i16: bool, p=None, frames_per_gp
     tot = torch.tensor([n_owned, ok, rx.rewalks], dtype=torch.int64, device=cdev)
     ofdm_dist.reduce_counters(tot, dist)
     tot = tot.cpu().numpy()
+    # per-phase device times, measured in this run: a few more calls (outside
+    # the timed region) with HIP events around the walk, resolve and decode
+    # (the events cost launch gaps, so the timed calls run without them)
+    phases = []
+    modem.stream_timing(True)
+    try:
+        for _ in range(3):
+            rx.run(walk, exchange)
+            phases.append(modem.last_stream_times())
+    except M.OfdmError:
+        phases = []  # no timed decode (e.g. a shard whose call took the halo walk)
+    finally:
+        modem.stream_timing(False)
+    torch.cuda.synchronize(dev)
     staged = None
     if staged_ab:
         modem.walk_tuning(staged_decode=1)
@@ -291,7 +305,7 @@ def stream_leg(args, dist, dev, world, rank, M, i16: bool, p=None, frames_per_gp
            "ms_per_call": elapsed / args.stream_reps * 1e3, "stream_samples": layout.n,
            "stream_GB": layout.n * esz / 1e9, "frames_sent": layout.total_frames, "frames_found": int(tot[0]),
            "frames_error_free": int(tot[1]), "rewalks_per_call": int(tot[2]) / args.stream_reps,
-           "halo": rx.halo, "tail": rx.tail,
+           "walk_halo": 0, "slice_halo": rx.own_lo - rx.slice_lo, "slice_tail": rx.slice_hi - rx.own_hi,
            "exchange_ms_per_call": exchange_ms,
            "roofline": {"bound": "hbm", "kernel": "whole stream pipeline (walker + compaction + fused decode, "
                                                   "host stitching overlapped)",
@@ -300,7 +314,7 @@ def stream_leg(args, dist, dev, world, rank, M, i16: bool, p=None, frames_per_gp
                         "algorithmic_bytes_per_call": alg_rank, "avg_call_ms": call_ms,
                         "traffic": (pmc or {}).get("hbm_bytes_per_call")},
            "cpu_baseline": None}
-    res["compute"] = decode_compute(p, n_owned, call_ms, workload)
+    res["compute"] = decode_compute(p, n_owned, call_ms, phases)
     if staged is not None:
         res["staged"] = staged
     if pipeline and world == 1 and args.stream_pipeline > 1:
@@ -343,39 +357,28 @@ def decode_flops_per_frame(p) -> int:
     return int(cfo + ffts + ramps + cps + emit)
 
 
-def load_stream_kernels(workload: str):
-    """Per-kernel mean times of the stream pipeline for this workload from the
-    committed rocprofv3 kernel-trace summary (profiles/stream_kernels_*.json,
-    made by tools/stream_kernels.py), or None."""
-    import glob
-    best = None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "stream_kernels_*.json"))):
-        try:
-            with open(path) as f:
-                d = json.load(f)
-        except (OSError, ValueError):
-            continue
-        if workload in d.get("workloads", {}):
-            best = dict(d["workloads"][workload], source=os.path.relpath(path, ROOT))
-    return best
-
-
-def decode_compute(p, frames: int, call_ms: float, workload: str) -> dict:
+def decode_compute(p, frames: int, call_ms: float, phases: list) -> dict:
     """The decode's compute side (VALU-bound: it takes about the same time
     with int16 input at a quarter of the bytes): useful FP64 flop/s over the
-    decode kernel's own time (its mean launch duration in the committed
-    kernel trace of this workload) against the FP64 vector peak; over the
-    whole call time when no trace is committed (a lower bound)."""
+    decode's own device time, measured in this run (HIP events around the
+    walk, resolve and decode of 3 calls after the timed ones,
+    ofdm_get_stream_timing), against the FP64 vector peak; over the whole
+    call time when no phase was timed (a lower bound)."""
     f = decode_flops_per_frame(p)
-    tr = load_stream_kernels(workload)
-    if tr and tr.get("decode_us"):
-        t_s, basis = tr["decode_us"] * 1e-6, f"decode kernel mean duration {tr['decode_us']:.1f} us ({tr['source']})"
+    if phases:
+        mean = {k: float(np.mean([ph[k] for ph in phases])) * 1e3 for k in phases[0]}
+        kus = {k.replace("_ms", "_us"): round(v, 1) for k, v in mean.items()}
+        kus["source"] = (f"this run: HIP events around each phase of {len(phases)} calls after the timed ones "
+                         "(ofdm_get_stream_timing; the events add launch gaps, so the phases sum above the "
+                         "timed call)")
+        t_s, basis = mean["decode_ms"] * 1e-6, f"decode phase {mean['decode_ms']:.1f} us, HIP events, this run"
     else:
-        t_s, basis = call_ms * 1e-3, "whole call time (walk + resolve + decode): no committed trace"
+        kus = None
+        t_s, basis = call_ms * 1e-3, "whole call time (walk + resolve + decode): no phase timed"
     ach = f * frames / t_s / 1e12
     return {"bound": "valu", "flops_per_frame": f, "achieved": ach, "peak": FP64_VALU_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": ach / FP64_VALU_PEAK_TFLOPS, "time_basis": basis,
-            "kernels_us": tr}
+            "kernels_us": kus}
 
 
 def stream_pipelined(args, p, M, dev, modem, layout, rx, walk, outs, x, nsl, cap, i16, n_owned, exchange, SS):
@@ -397,7 +400,7 @@ def stream_pipelined(args, p, M, dev, modem, layout, rx, walk, outs, x, nsl, cap
         outl.append(o2)
         rxs.append(r2)
         walks.append(SS.hip_walker(m2, x, nsl, r2.own_lo - r2.slice_lo, r2.own_hi - r2.slice_lo, cap, o2, i16=i16,
-                                   stream=st2))
+                                   stream=st2, report_cap=r2.cap))
     for i in range(P):
         rxs[i].run(walks[i], exchange)
     torch.cuda.synchronize(dev)

@@ -24,6 +24,16 @@
 #include <vector>
 
 #include "../../include/ofdm_mi355x.h"
+
+// RCCL's types and enum values for the one collective (ofdm_reduce_counters):
+// from its header where the build host has it; the library itself is loaded
+// at first use, so the core library neither links RCCL nor needs it to run
+#if __has_include(<rccl/rccl.h>)
+#include <rccl/rccl.h>
+static constexpr int kRcclInt64 = ncclInt64, kRcclSum = ncclSum;
+#else
+static constexpr int kRcclInt64 = 4, kRcclSum = 0;  // rccl.h: ncclInt64, ncclSum (header absent at build time)
+#endif
 #include "ofdm_internal.hpp"
 #include "ofdm_sync.hpp"
 
@@ -189,6 +199,12 @@ struct ofdm_ctx {
     // and the resolve kernel's status block (page-locked, written by the kernel)
     Grow s_pub, s_chain, h_status;
     bool pub_zero = false;         // every s_pub word is zero
+    // per-phase device times of the last look-back stream call
+    // (ofdm_set_stream_timing): events before the walk, after the walk, after
+    // the resolve and after the decode, on the call's stream
+    bool phase_timing = false;
+    bool phase_valid = false;
+    hipEvent_t ev_phase[4] = {};
 
     ofdm::DevTables tables(bool bpsk) const
     {
@@ -342,6 +358,8 @@ int ofdm_destroy(ofdm_ctx* c)
     if (c->ev_walk) (void)hipEventDestroy(c->ev_walk);
     if (c->ev_wdone) (void)hipEventDestroy(c->ev_wdone);
     if (c->side) (void)hipStreamDestroy(c->side);
+    for (hipEvent_t ev : c->ev_phase)
+        if (ev) (void)hipEventDestroy(ev);
     for (auto& pl : c->cfo_plans) {
         if (pl.tw_sub) (void)hipFree(pl.tw_sub);
         if (pl.tw_full) (void)hipFree(pl.tw_full);
@@ -1426,9 +1444,12 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     // (chunk 0 walks in from `start`, the others a halo before their core).
     // A look-back walker may walk on through the next core too (its walk met
     // no record of that chunk's); one more overflows: the host falls back
-    const int max_rec =
+    int max_rec =
         (int)(((lbk ? 2 : 1) * chunk + std::max(halo, own_lo - start) + std::max(ext, 2 * flen) + ofdm::WALK_SCAN_MAX +
                2 * c->p.t2sin_size + c->p.pr_sin_len) / msg + (lbk ? 8 : 4));
+    // test hook: a smaller record buffer makes look-back walkers overflow
+    // (the halo walk, which the cap does not touch, then takes the call)
+    if (lbk && tu.max_rec_cap > 0) max_rec = std::min(max_rec, tu.max_rec_cap);
     int rc;
     const size_t rec_b = (size_t)nchunks * max_rec * sizeof(long);
     // layout: records | exit states | exit ring ends | re-walk start (pos, ring end) | counts | ...
@@ -1541,8 +1562,12 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     long* d_prof = nullptr;
     if (prof_path) HIP_TRY(hipMalloc((void**)&d_prof, (size_t)nchunks * ofdm::WALK_PROF_FIELDS * sizeof(long)));
     w.prof = d_prof;
+    c->phase_valid = false;
+    const bool timed = c->phase_timing && lbk;  // events between the kernels: measurement calls only
+    if (timed) HIP_TRY(hipEventRecord(c->ev_phase[0], st));
     hipError_t e = ofdm::launch_stream_walk(c->t2_logn, w, std::min(nchunks, slots), st);
     if (e != hipSuccess) return hip_fail(e, "stream_walk launch");
+    if (timed) HIP_TRY(hipEventRecord(c->ev_phase[1], st));
     if (d_prof) {
         std::vector<long> hp((size_t)nchunks * ofdm::WALK_PROF_FIELDS);
         HIP_TRY(hipStreamSynchronize(st));
@@ -1730,8 +1755,13 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
         if (e != hipSuccess) return hip_fail(e, "stream resolve launch");
         c->pub_zero = true;    // cleared by the resolve (stream order)
         c->queue_zero = true;  // likewise the chunk counter
+        if (timed) HIP_TRY(hipEventRecord(c->ev_phase[2], st));
         const bool spec = fused && ub > 0 && ub * per <= ((size_t)256 << 20);
         if (spec && (rc = decode_fused(d_pbs, ub, d_pbs + ub))) return rc;
+        if (timed && spec) {
+            HIP_TRY(hipEventRecord(c->ev_phase[3], st));
+            c->phase_valid = true;
+        }
         // the resolve kernel's last word is the flags word of the status:
         // poll it (no event between the resolve and the decode: a marker
         // between two dependent kernels costs a launch gap); if it has not
@@ -2028,7 +2058,8 @@ int ofdm_set_walk_tuning(ofdm_ctx* c, const ofdm_walk_tuning* t)
     if (!c || !t) return fail(OFDM_ERR_INVALID, "null argument");
     if (t->staged_decode != 0 && t->staged_decode != 1) return fail(OFDM_ERR_INVALID, "staged_decode must be 0 or 1");
     if (t->lookback != 0 && t->lookback != 1) return fail(OFDM_ERR_INVALID, "lookback must be 0 or 1");
-    if (t->chunks_per_slot < 1 || t->halo_milli < -1 || t->ext_milli < 0 || !(t->t2_margin >= 0.0))
+    if (t->chunks_per_slot < 1 || t->halo_milli < -1 || t->ext_milli < 0 || !(t->t2_margin >= 0.0) ||
+        t->max_rec_cap < 0)
         return fail(OFDM_ERR_INVALID, "walk tuning out of range");
     if (t->t2_margin < 4e-5 && !t->allow_uncertified)
         return fail(OFDM_ERR_INVALID, "t2_margin %g is below the certified 4e-5 (the walk could differ from the "
@@ -2047,6 +2078,30 @@ int ofdm_rx_stream_shard(ofdm_ctx* c, const double* iq, const int16_t* iq16, siz
     if (!c || !start) return fail(OFDM_ERR_INVALID, "null argument");
     return rx_stream_impl(c, iq, iq16, n, max_frames, chunk, pb_out, bytes_out, constell_out, cfo_out, nframes_out,
                           stream, *start, own_lo, own_hi, located, located_lag, located_cap, nlocated_out, exit_out);
+}
+
+int ofdm_set_stream_timing(ofdm_ctx* c, int on)
+{
+    if (!c || (on != 0 && on != 1)) return fail(OFDM_ERR_INVALID, "need a ctx and on = 0 or 1");
+    HIP_TRY(hipSetDevice(c->device));
+    for (hipEvent_t& ev : c->ev_phase)
+        if (on && !ev) HIP_TRY(hipEventCreate(&ev));
+    c->phase_timing = on != 0;
+    c->phase_valid = false;
+    return OFDM_OK;
+}
+
+int ofdm_get_stream_timing(ofdm_ctx* c, float* walk_ms, float* resolve_ms, float* decode_ms)
+{
+    if (!c || !walk_ms || !resolve_ms || !decode_ms) return fail(OFDM_ERR_INVALID, "null argument");
+    if (!c->phase_valid)
+        return fail(OFDM_ERR_INVALID, "no timed call: ofdm_set_stream_timing(ctx, 1), then a look-back stream call "
+                                      "whose decode runs behind the resolve");
+    HIP_TRY(hipEventSynchronize(c->ev_phase[3]));
+    HIP_TRY(hipEventElapsedTime(walk_ms, c->ev_phase[0], c->ev_phase[1]));
+    HIP_TRY(hipEventElapsedTime(resolve_ms, c->ev_phase[1], c->ev_phase[2]));
+    HIP_TRY(hipEventElapsedTime(decode_ms, c->ev_phase[2], c->ev_phase[3]));
+    return OFDM_OK;
 }
 
 int ofdm_stream_initial_state(const ofdm_ctx* c, ofdm_walk_state* out)
@@ -2119,8 +2174,7 @@ int ofdm_reduce_counters(ofdm_ctx* c, int64_t* counters, size_t count, void* com
         }
     }
     HIP_TRY(hipSetDevice(c->device));
-    constexpr int kInt64 = 4, kSum = 0;  // rccl.h: ncclInt64, ncclSum
-    const int r = all_reduce(counters, counters, count, kInt64, kSum, comm, (hipStream_t)stream);
+    const int r = all_reduce(counters, counters, count, kRcclInt64, kRcclSum, comm, (hipStream_t)stream);
     if (r != 0) return fail(OFDM_ERR_HIP, "ncclAllReduce: %s", err_str ? err_str(r) : "error");
     return OFDM_OK;
 }

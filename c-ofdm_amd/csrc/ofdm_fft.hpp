@@ -24,8 +24,31 @@
 // would add vmcnt(0) and drain that prefetch).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <cfloat>
+
+// Phase markers for the annotated-ISA instruction count (tools/isa_phases.py,
+// built with -DOFDM_PHASE_MARKS): an assembler comment naming the phase that
+// starts there. Empty in the product build.
+#ifdef OFDM_PHASE_MARKS
+#define OFDM_PHASE(name) asm volatile("; OFDM_PHASE " #name)
+#else
+#define OFDM_PHASE(name) ((void)0)
+#endif
 
 namespace ofdm {
+
+// Diagnostics build of the fused stream decode (stream_decode_kernel<.., true>,
+// selected by OFDM_DECODE_STOP=k): every wave ends at stop point k, so SQ
+// counters of runs with k = 1, 2, ... give each segment's executed
+// instructions by difference (tools/decode_phase_counts.sh). Never set in
+// the product path; the product instantiation has no checks.
+static __device__ int g_decode_stop = 1 << 30;
+#define OFDM_STOP(PROF, k)                                                   \
+    do {                                                                     \
+        if constexpr (PROF) {                                                \
+            if ((k) >= g_decode_stop) __builtin_amdgcn_endpgm();             \
+        }                                                                    \
+    } while (0)
 
 // ---------------------------------------------------------------- complex
 __device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
@@ -72,6 +95,49 @@ __device__ __forceinline__ double2 cmul_exact(double2 a, double2 b)
                         add_rn(mul_rn(a.x, b.y), mul_rn(a.y, b.x)));
 }
 
+// atan2 for the stream decode's phases (carg of a complex sum: cp_freq_sinh,
+// pr_phase_sinh, chan_char_lq's per-carrier angles; Frame.hpp:238-274,
+// 397-405), within 3 ulp of the correctly rounded value (the stream's 1e-9
+// parity bar; measured 2.5 ulp worst over 2e5 random arguments against a
+// 50-digit atan2), branch-free, about 45 VALU instructions against the math
+// library's ~105. Octant reduction to |u| <= tan(pi/8) with one division
+// (u = n/d, or (n - d)/(n + d) and pi/4 added), then atan(u) = u + u z P(z),
+// z = u^2, P of degree 10 (a Chebyshev-node fit with 2e-18 absolute error
+// on [0, tan^2(pi/8)]). IEEE special cases by selects: zeros (+-0 or +-pi
+// by the signs), infinities (multiples of pi/4), NaN.
+__device__ __forceinline__ double atan2_fast(double y, double x)
+{
+    double ax = fabs(x), ay = fabs(y);
+    const bool ix = ax > DBL_MAX, iy = ay > DBL_MAX;  // infinite (NaN compares false)
+    if (ix || iy) {  // the direction of the infinite argument(s)
+        ax = ix ? 1.0 : 0.0;
+        ay = iy ? 1.0 : 0.0;
+    }
+    const bool sw = ay > ax;
+    const double n = sw ? ax : ay, d0 = sw ? ay : ax;  // n <= d
+    const double d = d0 > 0.0 ? d0 : 1.0;              // both zero: u = 0
+    const bool hi = n > d * 0.41421356237309503;       // tan(pi/8)
+    const double u = hi ? (n - d) / (n + d) : n / d;
+    const double z = u * u;
+    double p = -0.01917688711906226;
+    p = __builtin_fma(p, z, 0.03923165829558719);
+    p = __builtin_fma(p, z, -0.0508544973794026);
+    p = __builtin_fma(p, z, 0.0585814891280221);
+    p = __builtin_fma(p, z, -0.06664511447381948);
+    p = __builtin_fma(p, z, 0.07692183190826087);
+    p = __builtin_fma(p, z, -0.09090904578123903);
+    p = __builtin_fma(p, z, 0.11111111015256361);
+    p = __builtin_fma(p, z, -0.14285714284666542);
+    p = __builtin_fma(p, z, 0.1999999999999552);
+    p = __builtin_fma(p, z, -0.3333333333333333);
+    double r = __builtin_fma(u * z, p, u);
+    if (hi) r += 0.78539816339744830962;  // pi/4
+    if (sw) r = 1.5707963267948966192 - r;
+    if (__builtin_signbit(x)) r = 3.1415926535897932385 - r;
+    r = copysign(r, y);
+    return (x != x || y != y) ? x + y : r;
+}
+
 // cp_freq_sinh's symbol phase carg(sum_j conj(x_j) x_{j+N}) over the
 // freq-shifted samples (Frame.hpp:238-263), from the sum acc over the raw
 // samples times the shift's phasor rot. The reference's sum starts at +0, so
@@ -81,7 +147,7 @@ __device__ __forceinline__ double cp_phase(double2 acc, double2 rot)
 {
     if (acc.x == 0.0 && acc.y == 0.0) return 0.0;
     const double2 r = cmul_exact(acc, rot);
-    return atan2(r.y, r.x);
+    return atan2_fast(r.y, r.x);
 }
 
 // libgcc __divdc3 (Smith's algorithm) for finite operands — what the

@@ -9,6 +9,8 @@
 // holds x[t + T*i], T = N/8 <= 64, LDS image XOR-swizzled), on float2: half
 // the registers, LDS bytes and VALU cycles per block.
 #pragma once
+#include <type_traits>
+
 #include "ofdm_fft.hpp"
 
 namespace ofdm {
@@ -141,69 +143,103 @@ __device__ __forceinline__ void fft_regs_wave32(float2 (&v)[8], int t, const dou
 
 namespace ofdm {
 
-// ---------------------------------------------------------------- two blocks at once
-// Two FP32 transforms in lockstep, element = float4 {A.re, A.im, B.re, B.im}:
-// the LDS image holds 16-B elements, so ofdm_fft.hpp's swizzle (built for
-// 16-B accesses) keeps every pass conflict-free, and one ds_read/ds_write_b128
-// moves a value of both blocks (a float2 image with that swizzle conflicted
-// 4-way on the stride-8 writes).
-__device__ __forceinline__ float4 q_add(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
-__device__ __forceinline__ float4 q_sub(float4 a, float4 b) { return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w); }
-__device__ __forceinline__ float4 q_mulw(float4 a, float2 w)  // both halves times w
-{
-    return make_float4(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x, a.z * w.x - a.w * w.y, a.z * w.y + a.w * w.x);
-}
-template <int SIGN>
-__device__ __forceinline__ float4 q_mul_j(float4 a)
-{
-    return SIGN > 0 ? make_float4(-a.y, a.x, -a.w, a.z) : make_float4(a.y, -a.x, a.w, -a.z);
-}
-__device__ __forceinline__ float4 q_scale(float4 a, float c) { return make_float4(a.x * c, a.y * c, a.z * c, a.w * c); }
+// ---------------------------------------------------------------- two blocks at once, packed
+// Two FP32 transforms in lockstep, structure-of-arrays: a point is the pair
+// re = {A.re, B.re}, im = {A.im, B.im} (pf2 = two packed floats), so every
+// add, subtract and twiddle product of the two blocks is one gfx950 packed
+// instruction (v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32, the twiddle a
+// broadcast operand): half the VALU issue of two unpacked transforms. The LDS
+// image holds 16-B elements {A.re, B.re, A.im, B.im}, so ofdm_fft.hpp's
+// swizzle (built for 16-B accesses) keeps every pass conflict-free and one
+// ds_read/ds_write_b128 moves a point of both blocks.
+typedef float pf2 __attribute__((ext_vector_type(2)));
 
-template <int SIGN>
-__device__ __forceinline__ void qdft2(float4& a, float4& b)
-{
-    const float4 t = a;
-    a = q_add(t, b);
-    b = q_sub(t, b);
-}
+struct PCx {
+    pf2 re, im;
+};
 
-template <int SIGN>
-__device__ __forceinline__ void qdft4(float4& a0, float4& a1, float4& a2, float4& a3)
+__device__ __forceinline__ PCx p_add(PCx a, PCx b) { return {a.re + b.re, a.im + b.im}; }
+__device__ __forceinline__ PCx p_sub(PCx a, PCx b) { return {a.re - b.re, a.im - b.im}; }
+// both blocks times the complex scalar w
+__device__ __forceinline__ PCx p_mulw(PCx a, float2 w)
 {
-    const float4 t0 = q_add(a0, a2), t1 = q_sub(a0, a2);
-    const float4 t2 = q_add(a1, a3), t3 = q_mul_j<SIGN>(q_sub(a1, a3));
-    a0 = q_add(t0, t2);
-    a1 = q_add(t1, t3);
-    a2 = q_sub(t0, t2);
-    a3 = q_sub(t1, t3);
+    const pf2 wr = {w.x, w.x}, wi = {w.y, w.y};
+    return {a.re * wr - a.im * wi, a.re * wi + a.im * wr};
+}
+template <int SIGN>
+__device__ __forceinline__ PCx p_mul_j(PCx a)  // a * (SIGN i)
+{
+    return SIGN > 0 ? PCx{-a.im, a.re} : PCx{a.im, -a.re};
 }
 
 template <int SIGN>
-__device__ __forceinline__ void qdft8(float4& x0, float4& x1, float4& x2, float4& x3, float4& x4, float4& x5,
-                                      float4& x6, float4& x7)
+__device__ __forceinline__ void pdft2(PCx& a, PCx& b)
+{
+    const PCx t = a;
+    a = p_add(t, b);
+    b = p_sub(t, b);
+}
+
+template <int SIGN>
+__device__ __forceinline__ void pdft4(PCx& a0, PCx& a1, PCx& a2, PCx& a3)
+{
+    const PCx t0 = p_add(a0, a2), t1 = p_sub(a0, a2);
+    const PCx t2 = p_add(a1, a3), t3 = p_mul_j<SIGN>(p_sub(a1, a3));
+    a0 = p_add(t0, t2);
+    a1 = p_add(t1, t3);
+    a2 = p_sub(t0, t2);
+    a3 = p_sub(t1, t3);
+}
+
+template <int SIGN>
+__device__ __forceinline__ void pdft8(PCx& x0, PCx& x1, PCx& x2, PCx& x3, PCx& x4, PCx& x5, PCx& x6, PCx& x7)
 {
     constexpr float C = 0.70710678118654752440f;
-    qdft4<SIGN>(x0, x2, x4, x6);
-    qdft4<SIGN>(x1, x3, x5, x7);
-    // O1 *= W8, O2 *= W8^2 = SIGN*i, O3 *= W8^3
-    const float4 o1 = q_scale(q_add(x3, q_mul_j<SIGN>(x3)), C);
-    const float4 o2 = q_mul_j<SIGN>(x5);
-    const float4 o3 = q_scale(q_sub(q_mul_j<SIGN>(x7), x7), C);
-    const float4 e0 = x0, e1 = x2, e2 = x4, e3 = x6, o0 = x1;
-    x0 = q_add(e0, o0);
-    x4 = q_sub(e0, o0);
-    x1 = q_add(e1, o1);
-    x5 = q_sub(e1, o1);
-    x2 = q_add(e2, o2);
-    x6 = q_sub(e2, o2);
-    x3 = q_add(e3, o3);
-    x7 = q_sub(e3, o3);
+    const pf2 c2 = {C, C};
+    pdft4<SIGN>(x0, x2, x4, x6);
+    pdft4<SIGN>(x1, x3, x5, x7);
+    // O1 *= W8 = C (1 + SIGN i), O2 *= SIGN i, O3 *= W8^3 = C (-1 + SIGN i)
+    const PCx o1 = SIGN > 0 ? PCx{(x3.re - x3.im) * c2, (x3.im + x3.re) * c2}
+                            : PCx{(x3.re + x3.im) * c2, (x3.im - x3.re) * c2};
+    const PCx o2 = p_mul_j<SIGN>(x5);
+    const PCx o3 = SIGN > 0 ? PCx{-(x7.re + x7.im) * c2, (x7.re - x7.im) * c2}
+                            : PCx{(x7.im - x7.re) * c2, -(x7.re + x7.im) * c2};
+    const PCx e0 = x0, e1 = x2, e2 = x4, e3 = x6, o0 = x1;
+    x0 = p_add(e0, o0);
+    x4 = p_sub(e0, o0);
+    x1 = p_add(e1, o1);
+    x5 = p_sub(e1, o1);
+    x2 = p_add(e2, o2);
+    x6 = p_sub(e2, o2);
+    x3 = p_add(e3, o3);
+    x7 = p_sub(e3, o3);
 }
 
+// Sum over aligned groups of G lanes (G = 2..64, a power of two), valid in
+// every lane of the group: DPP row permutations (xor 1, xor 2, the 8-lane
+// half-mirror, the 16-lane mirror; each folds into the add as a DPP
+// operand, no LDS) up to 16 lanes, then ds_swizzle / bpermute shuffles.
+template <int G>
+__device__ __forceinline__ float group_sum(float v)
+{
+    auto dpp = [](float x, auto ctrl) {
+        return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), decltype(ctrl)::value, 0xf, 0xf, false));
+    };
+    if constexpr (G >= 2) v += dpp(v, std::integral_constant<int, 0xB1>{});   // quad_perm [1,0,3,2]
+    if constexpr (G >= 4) v += dpp(v, std::integral_constant<int, 0x4E>{});   // quad_perm [2,3,0,1]
+    if constexpr (G >= 8) v += dpp(v, std::integral_constant<int, 0x141>{});  // row_half_mirror
+    if constexpr (G >= 16) v += dpp(v, std::integral_constant<int, 0x140>{}); // row_mirror
+    if constexpr (G >= 32) v += __shfl_xor(v, 16);
+    if constexpr (G >= 64) v += __shfl_xor(v, 32);
+    return v;
+}
+
+__device__ __forceinline__ float4 p_pack(PCx a) { return make_float4(a.re.x, a.re.y, a.im.x, a.im.y); }
+__device__ __forceinline__ PCx p_unpack(float4 v) { return {pf2{v.x, v.y}, pf2{v.z, v.w}}; }
+
 template <int LOGN, int R, int NS, int SIGN>
-__device__ __forceinline__ void stockham_pass32x2(float4 (&v)[8], int t, const double2* __restrict__ lds_tw,
-                                                  float4* __restrict__ lds, bool write)
+__device__ __forceinline__ void stockham_pass32p(PCx (&v)[8], int t, const double2* __restrict__ lds_tw,
+                                                 float4* __restrict__ lds, bool write)
 {
     constexpr int N = 1 << LOGN, T = N / 8, B = 8 / R;
 #pragma unroll
@@ -211,34 +247,36 @@ __device__ __forceinline__ void stockham_pass32x2(float4 (&v)[8], int t, const d
         const int b = t + T * u;
         const int k = b & (NS - 1);
         if constexpr (NS > 1) {
+            // the base twiddle from the FP64 table (TwLds), rounded once;
+            // its powers by a running product (scalar: one per butterfly)
             const double2 w64 = tw_get<LOGN, N / R>(lds_tw, k * (N / (NS * R)));
             float2 w1 = make_float2((float)w64.x, (float)w64.y);
             if (SIGN > 0) w1.y = -w1.y;
             float2 w = w1;
-            v[u + B] = q_mulw(v[u + B], w1);
+            v[u + B] = p_mulw(v[u + B], w1);
 #pragma unroll
             for (int r = 2; r < R; ++r) {
                 w = fmulc(w, w1);
-                v[u + r * B] = q_mulw(v[u + r * B], w);
+                v[u + r * B] = p_mulw(v[u + r * B], w);
             }
         }
         if constexpr (R == 8)
-            qdft8<SIGN>(v[u], v[u + B], v[u + 2 * B], v[u + 3 * B], v[u + 4 * B], v[u + 5 * B], v[u + 6 * B],
+            pdft8<SIGN>(v[u], v[u + B], v[u + 2 * B], v[u + 3 * B], v[u + 4 * B], v[u + 5 * B], v[u + 6 * B],
                         v[u + 7 * B]);
         else if constexpr (R == 4)
-            qdft4<SIGN>(v[u], v[u + B], v[u + 2 * B], v[u + 3 * B]);
+            pdft4<SIGN>(v[u], v[u + B], v[u + 2 * B], v[u + 3 * B]);
         else
-            qdft2<SIGN>(v[u], v[u + B]);
+            pdft2<SIGN>(v[u], v[u + B]);
         if (!write) continue;
         const int idxD = (b - k) * R + k;
 #pragma unroll
-        for (int r = 0; r < R; ++r) lds[lds_swz(idxD + r * NS)] = v[u + r * B];
+        for (int r = 0; r < R; ++r) lds[lds_swz(idxD + r * NS)] = p_pack(v[u + r * B]);
     }
 }
 
 template <int LOGN, int PASS, int SIGN>
-__device__ __forceinline__ void fft_regs_tail_wave32x2(float4 (&v)[8], int t, const double2* __restrict__ lds_tw,
-                                                       float4* __restrict__ lds)
+__device__ __forceinline__ void fft_regs_tail_wave32p(PCx (&v)[8], int t, const double2* __restrict__ lds_tw,
+                                                      float4* __restrict__ lds)
 {
     using S = FftShape<LOGN>;
     constexpr int T = S::T;
@@ -249,25 +287,26 @@ __device__ __forceinline__ void fft_regs_tail_wave32x2(float4 (&v)[8], int t, co
     constexpr bool LAST = PASS == NPASS - 1;
     wave_lds_sync();  // previous pass fully written
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = lds[lds_swz(t + T * i)];
+    for (int i = 0; i < 8; ++i) v[i] = p_unpack(lds[lds_swz(t + T * i)]);
     if constexpr (LAST) {
-        stockham_pass32x2<LOGN, R, NS, SIGN>(v, t, lds_tw, lds, false);
+        stockham_pass32p<LOGN, R, NS, SIGN>(v, t, lds_tw, lds, false);
     } else {
         wave_lds_sync();  // every lane has read before the image is overwritten
-        stockham_pass32x2<LOGN, R, NS, SIGN>(v, t, lds_tw, lds, true);
-        fft_regs_tail_wave32x2<LOGN, PASS + 1, SIGN>(v, t, lds_tw, lds);
+        stockham_pass32p<LOGN, R, NS, SIGN>(v, t, lds_tw, lds, true);
+        fft_regs_tail_wave32p<LOGN, PASS + 1, SIGN>(v, t, lds_tw, lds);
     }
 }
 
-// Two N-point FP32 transforms (v[i] = {a[t + T*i], b[t + T*i]}) by T <= 64
-// threads of one wave, image lds (N float4); on exit v[i] = {A, B}[t + T*i].
+// Two N-point FP32 transforms (v[i] = {a, b}[t + T*i] as packed re / im
+// pairs) by T <= 64 threads of one wave, image lds (N float4); on exit
+// v[i] = {A, B}[t + T*i].
 template <int LOGN, int SIGN>
-__device__ __forceinline__ void fft_regs_wave32x2(float4 (&v)[8], int t, const double2* __restrict__ lds_tw,
-                                                  float4* __restrict__ lds)
+__device__ __forceinline__ void fft_regs_wave32p(PCx (&v)[8], int t, const double2* __restrict__ lds_tw,
+                                                 float4* __restrict__ lds)
 {
     static_assert(LOGN >= 6 && LOGN <= 9, "N/8 <= one wave");
-    stockham_pass32x2<LOGN, 8, 1, SIGN>(v, t, lds_tw, lds, true);
-    fft_regs_tail_wave32x2<LOGN, 1, SIGN>(v, t, lds_tw, lds);
+    stockham_pass32p<LOGN, 8, 1, SIGN>(v, t, lds_tw, lds, true);
+    fft_regs_tail_wave32p<LOGN, 1, SIGN>(v, t, lds_tw, lds);
 }
 
 }  // namespace ofdm

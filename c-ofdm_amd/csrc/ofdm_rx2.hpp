@@ -60,7 +60,7 @@ __host__ __device__ constexpr int rt_size(int S) { return RT_PER_SYM * S + 3; } 
 // transforms and stored to L.chl after the gains (loads issued among the
 // emit's stores would wait for them). Every thread of the 128-thread
 // workgroup calls it; it returns after a barrier (LDS reusable).
-template <bool I16, bool TAB = false>
+template <bool I16, bool TAB = false, bool PROF = false>
 __device__ __forceinline__ void rx2_frame(const RxArgs& a, long f, const Rx2Lds& L, const double* corr,
                                           const int (&pk0)[RX_DPT], int pbin, const double2* chan_g = nullptr)
 {
@@ -106,6 +106,7 @@ __device__ __forceinline__ void rx2_frame(const RxArgs& a, long f, const Rx2Lds&
     for (int q = 0; q < SH; ++q) {
         const int s = 2 * q + w;
         if (s < S) {  // uniform
+            OFDM_PHASE(rx_symbol);
             asm volatile("" ::: "memory");
             int lq;
             asm volatile("v_mov_b32 %0, %1" : "=v"(lq) : "v"(lane));
@@ -155,7 +156,9 @@ __device__ __forceinline__ void rx2_frame(const RxArgs& a, long f, const Rx2Lds&
                     if (i < 7) c = cmul(c, wr);
                 }
             }
+            OFDM_PHASE(rx_symbol_fft);
             fft_block_wave<LOGN, -1>(v, lq, L.tw, img);
+            OFDM_PHASE(rx_symbol_gather);
             if (lq < P) L.pil[s * P + lq] = img[pbin];
 #pragma unroll
             for (int i = 0; i < RX_DPT; ++i) y[q][i] = img[pk[i] & 0xffff];
@@ -163,6 +166,8 @@ __device__ __forceinline__ void rx2_frame(const RxArgs& a, long f, const Rx2Lds&
         }
     }
     __syncthreads();  // both waves' pilots visible; the images are free
+    OFDM_STOP(PROF, 3);
+    OFDM_PHASE(rx_chan_line);
     // two named registers, not an array (an array held across the barriers
     // below went to scratch)
     double2 chv0 = make_double2(0.0, 0.0), chv1 = make_double2(0.0, 0.0);
@@ -190,6 +195,7 @@ __device__ __forceinline__ void rx2_frame(const RxArgs& a, long f, const Rx2Lds&
     }
     // phys_pilot_ampl = sum |pilot| / (P*S*pilot_ampl)   (Frame.cpp:76-80),
     // summed by wave 0 in rx_kernel's lane order
+    OFDM_PHASE(rx_phys_gains);
     if (w == 0) {
         double acc = 0.0;
         for (int i = lane; i < S * P; i += T) acc += hypot(L.pil[i].x, L.pil[i].y);
@@ -215,6 +221,8 @@ __device__ __forceinline__ void rx2_frame(const RxArgs& a, long f, const Rx2Lds&
         if (tid + 128 < D) L.chl[tid + 128] = chv1;
     }
     __syncthreads();
+    OFDM_STOP(PROF, 4);
+    OFDM_PHASE(rx_emit);
     auto emit = [&](int s, const double2 (&yw)[RX_DPT]) {
         double2* cbase = a.constell ? a.constell + (f * S + s) * D : nullptr;
 #pragma unroll
@@ -235,6 +243,8 @@ __device__ __forceinline__ void rx2_frame(const RxArgs& a, long f, const Rx2Lds&
         if (s < S) emit(s, y[q]);  // uniform
     }
     __syncthreads();  // decisions visible
+    OFDM_STOP(PROF, 5);
+    OFDM_PHASE(rx_pack);
     if (a.bytes) {
         if (by_word) {
             const int per_word = 32 / a.k;  // decisions per output word
@@ -263,6 +273,7 @@ __device__ __forceinline__ void rx2_frame(const RxArgs& a, long f, const Rx2Lds&
         }
     }
     __syncthreads();  // dec / pil / gain / chl are rewritten by the next frame
+    OFDM_PHASE(rx_end);
 }
 
 }  // namespace ofdm

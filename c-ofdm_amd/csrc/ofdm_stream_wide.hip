@@ -362,7 +362,7 @@ __global__ void __launch_bounds__(WideGeo<LOGN>::NT, 4) stream_decode_wide_kerne
             acc = cadd(acc, make_double2(bacc.x * isn, bacc.y * isn));
         }
         acc = block_sum2<NT>(acc, red);  // group 1 adds zeros
-        const double phr = atan2(acc.y, acc.x);
+        const double phr = atan2_fast(acc.y, acc.x);
         // e^{-i phr} = conj(acc) / |acc| (uniform; sincos for a zero or non-finite sum)
         double2 rot;
         const double ha = hypot(acc.x, acc.y);
@@ -404,7 +404,7 @@ __global__ void __launch_bounds__(WideGeo<LOGN>::NT, 4) stream_decode_wide_kerne
                 const double2 fs = make_double2(dat[tid].x / phys, dat[tid].y / phys);
                 q = cdiv_exact(cdiv_exact(fs, coef), mp);
             }
-            ph[tid] = atan2(q.y, q.x);
+            ph[tid] = atan2_fast(q.y, q.x);
         }
     }
     __syncthreads();

@@ -1070,7 +1070,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 3) stream_params_kernel(Strea
         const double isn = 1.0 / sqrt((double)N);
         acc = cadd(acc, make_double2(bacc.x * isn, bacc.y * isn));
         acc = block_sum2<T>(acc, red);
-        if (t == 0) phpr = atan2(acc.y, acc.x);
+        if (t == 0) phpr = atan2_fast(acc.y, acc.x);
         __syncthreads();
         phr = phpr;
         double rs2, rc2;
@@ -1095,7 +1095,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 8, 3) stream_params_kernel(Strea
             const double2 coef = cdiv_exact(p0, p0);
             const double2 fs = make_double2(dat[i].x / phys, dat[i].y / phys);
             const double2 q = cdiv_exact(cdiv_exact(fs, coef), mpre[u]);
-            ph[i] = atan2(q.y, q.x);
+            ph[i] = atan2_fast(q.y, q.x);
         }
     }
     __syncthreads();
@@ -1206,7 +1206,7 @@ struct SyncLds {
 // frame's ramp / channel table (ofdm_rx2.hpp rt_size) to rt, in LDS over the
 // stage's small arrays; returns after a barrier. load_tw: fill the twiddle
 // tables here (else they are resident and visible).
-template <bool I16>
+template <bool I16, bool PROF = false>
 __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsArgs& a, long f, const SyncLds& Ls,
                                            double2* rt, bool load_tw)
 {
@@ -1233,6 +1233,7 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const long x0 = a.starts[f];
     const int half = a.D / 2, Q = 1 + a.S;
+    OFDM_PHASE(cfo_transforms);
     // ---------------------------------------------------------- pilot_freq_sinh (both waves)
     // transform g holds x[G*n + g], n = tt + 16*i: g = lane/16 (0..3) on
     // wave 0, g = 4 on wave 1's lanes 0..15
@@ -1252,6 +1253,7 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
         if (w == 0 || lane < 16) fft_block_wave<LOGM, -1>(v, tt, tw7, img + g * M);
         __syncthreads();  // the five transforms visible
     }
+    OFDM_PHASE(cfo_radix5);
     {
         // X[k + M*r] = sum_q W_S^{q k} W_G^{q r} F_q[k]; stored fftshifted:
         // shifted[i] = spec[(i + S/2) % S]  (Frame.hpp:300-305). The window
@@ -1302,6 +1304,7 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
         // strictly below the winner's, so the winner is hypot's first maximum.
         // Otherwise (near-ties, or a non-finite element) the group takes
         // hypot of its window, as cfo_kernel does.
+        OFDM_PHASE(cfo_argmax);
         constexpr int AG = 8;
         constexpr double SURE = 1.0 - 64.0 * 0x1.0p-53;
         // the P windows that count (window P/2 is skipped by the sum below),
@@ -1369,6 +1372,7 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
             if (act && l == 0) wsum[i] = lo < hi ? (first_nan ? lo : bi) : hi;
         }
         __syncthreads();  // window maxima visible
+        OFDM_PHASE(cfo_final);
         if (tid == 0) {
             double shift = 0.0;
             for (int i = 0; i <= c.P; ++i)
@@ -1380,11 +1384,13 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
             c.cfo_out[f] = shift;
         }
         __syncthreads();  // the CFO visible; the CFO images are free
+        OFDM_STOP(PROF, 1);
     }
     if (w == 0) {
         const double cfo = scal[0];
 
         // ---------------------------------------------------------- preamble (stream_params_kernel)
+        OFDM_PHASE(w0_pre_load);
         const int t = lane;
         int dbin[4], dslot[2];
         double2 mpre[4], prc[2];
@@ -1403,6 +1409,7 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
 #pragma unroll
         for (int r = 0; r < RMAX; ++r)
             z[r] = r < LT ? src_sample_t<I16>(a.iq, a.iq16, x0 + t + (long)T * r) : make_double2(0.0, 0.0);
+        OFDM_PHASE(w0_pre_cpsum);
         double rs, rc;
         sincospi(-2.0 * cfo * (double)N, &rs, &rc);
         {
@@ -1430,6 +1437,7 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
             // other's decode: int16 stream 183 -> 162 G samples/s in a
             // same-box A/B that reverted each part of that change alone,
             // profiles/r04h_pipelined_rev.json.)
+            OFDM_PHASE(w0_pre_ramp);
             double sn, cs, ws, wc;
             sincos(slope0 * (double)t, &sn, &cs);
             sincos(slope0 * (double)T, &ws, &wc);
@@ -1453,7 +1461,9 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
 #pragma unroll
             for (int i = 0; i < 8; ++i) vv[i] = fftb[t + T * i];
             wave_lds_sync();
+            OFDM_PHASE(w0_pre_fft);
             fft_block_wave<LOGN, -1>(vv, t, tw9, fftb);  // Z (unrotated)
+            OFDM_PHASE(w0_pre_phase);
             const double2 pz = t < a.P ? fftb[lds_swz(pbin)] : make_double2(0.0, 0.0);
             double2 dz[4];
             double2 bacc = make_double2(a.pilot_ampl * pz.x, a.pilot_ampl * pz.y);
@@ -1465,7 +1475,7 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
             const double isn = 1.0 / sqrt((double)N);
             acc = cadd(acc, make_double2(bacc.x * isn, bacc.y * isn));
             acc = block_sum2<T>(acc, red);
-            phr = atan2(acc.y, acc.x);
+            phr = atan2_fast(acc.y, acc.x);
             // e^{-i phr} = conj(acc) / |acc| (acc is uniform: a uniform
             // branch keeps sincos for a zero or non-finite sum)
             double2 rot;
@@ -1484,6 +1494,7 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
                 if (t + T * u < half) dat[t + T * u] = cmul_exact(dz[u], rot);
         }
         wave_lds_sync();
+        OFDM_PHASE(w0_pre_phys_atan);
         double acc = 0.0;
         for (int i = t; i < a.P; i += T) acc += hypot(pil[i].x, pil[i].y);
         acc = block_sum2<T>(make_double2(acc, 0.0), red).x;
@@ -1511,10 +1522,11 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
                     const double2 fs = make_double2(dat[i].x / phys, dat[i].y / phys);
                     q = cdiv_exact(cdiv_exact(fs, coef), mpre[u]);
                 }
-                ph[i] = atan2(q.y, q.x);
+                ph[i] = atan2_fast(q.y, q.x);
             }
         }
         wave_lds_sync();
+        OFDM_PHASE(w0_pre_unwrap_ls);
         unwrap_scan<T, true>(ph, half, reinterpret_cast<unsigned*>(red + 24));  // one-pass unwrap (Frame.hpp:407-414)
         double sxy = 0.0, sy = 0.0;
         for (int i = t; i < half; i += T) {
@@ -1533,6 +1545,7 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
     } else {
         // ---------------------------------------------------------- message CP sums (wave 1)
         // two symbols per iteration, so both symbols' CP loads are in flight together
+        OFDM_PHASE(w1_msg_cpsums);
         const int t = lane;
         for (int q = 1; q < Q; q += 2) {
             const bool two = q + 1 < Q;  // uniform
@@ -1569,6 +1582,7 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
         }
     }
     __syncthreads();  // cfo, phi[0..S], phr and the LS fit visible
+    OFDM_PHASE(ramp_table);
     const double cfo = scal[0], phr = scal[1], b = scal[2], aa = scal[3];
     if (tid == 0) {
         double acc = 0.0;
@@ -1602,6 +1616,8 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
     if (tid < nt) rt[tid] = val;
     if (tid == 0) rt[nt] = make_double2(b, aa);
     __syncthreads();  // the table visible; the stage's other LDS is free
+    OFDM_STOP(PROF, 2);
+    OFDM_PHASE(sync_end);
 }
 
 // ========================================================================
@@ -1621,7 +1637,7 @@ __device__ __forceinline__ void sync_frame(const CfoArgs& c, const StreamParamsA
 // over each other. The channel reciprocals go through the chan scratch (L2)
 // from the sync stage to the rx stage's emit.
 // ========================================================================
-template <bool I16>
+template <bool I16, bool PROF = false>
 __global__ void __launch_bounds__(128, 4) stream_decode_kernel(CfoArgs c, StreamParamsArgs a, RxArgs r)
 {
     extern __shared__ double2 smem[];
@@ -1666,9 +1682,9 @@ __global__ void __launch_bounds__(128, 4) stream_decode_kernel(CfoArgs c, Stream
     // rx stage of the CU's other frames (priority 1 vs 0: 498 -> 478 us;
     // 2 and 3 gain less)
     __builtin_amdgcn_s_setprio(1);
-    sync_frame<I16>(c, a, f, Ls, rt, true);
+    sync_frame<I16, PROF>(c, a, f, Ls, rt, true);
     __builtin_amdgcn_s_setprio(0);
-    rx2_frame<I16, true>(r, f, Lr, reinterpret_cast<const double*>(rt), pk, pbin);
+    rx2_frame<I16, true, PROF>(r, f, Lr, reinterpret_cast<const double*>(rt), pk, pbin);
 }
 
 static bool stream_sync_geometry(const CfoArgs& c, const StreamParamsArgs& a, int logn, int logm, int g)
@@ -1684,6 +1700,19 @@ static hipError_t decode_launch(const CfoArgs& c, const StreamParamsArgs& a, con
     const size_t rx_u = sizeof(double2) * ((size_t)a.S * a.P + std::max(a.S * a.P, rt_size(a.S))) + sizeof(double) * 2;
     const size_t sync_u = sizeof(double2) * (a.P + 32 + 1 + a.S) + sizeof(double) * 132 + sizeof(int) * (a.P + 2);
     const size_t shm = sizeof(double2) * (TwLds<9>::SIZE + 1024) + std::max(rx_u, sync_u);
+    // diagnostics: OFDM_DECODE_STOP=k runs the build whose waves end at stop
+    // point k (per-segment instruction counts from SQ counters)
+    static const int stop = [] {
+        const char* e = getenv("OFDM_DECODE_STOP");
+        return e ? atoi(e) : 0;
+    }();
+    if (stop > 0) {
+        static std::once_flag once;
+        std::call_once(once, [] { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_decode_stop), &stop, sizeof(int)); });
+        lds_opt_in((const void*)stream_decode_kernel<I16, true>, 160 * 1024);
+        hipLaunchKernelGGL((stream_decode_kernel<I16, true>), dim3((unsigned)a.nframes), dim3(128), shm, st, c, a, r);
+        return hipGetLastError();
+    }
     lds_opt_in((const void*)stream_decode_kernel<I16>, 160 * 1024);
     hipLaunchKernelGGL(stream_decode_kernel<I16>, dim3((unsigned)a.nframes), dim3(128), shm, st, c, a, r);
     return hipGetLastError();
@@ -2287,7 +2316,11 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
     // look-back link {chunk this walk joins, the shared frame's index here and
     // there}: none until the walk joins one
     if (lb && t0 == 0) {
+        // all three words: the scratch is reused across calls of other
+        // layouts, and the resolve reads them for every chunk
         a.link[3 * c] = -1;
+        a.link[3 * c + 1] = 0;
+        a.link[3 * c + 2] = 0;
         __hip_atomic_store(a.pub + c, WALK_PUB_STARTED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // diagnostics (a.prof): stored as they happen, nothing held in registers
@@ -2458,6 +2491,18 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
                 // uncertain, the step is evaluated again in FP64.
                 float4* fftb32 = reinterpret_cast<float4*>(big);  // one image per group, both blocks
                 const float lev = (float)a.t2_level, marg = (float)a.t2_margin;
+                // detector-bin weights of this thread's 8 bins k = tt + T*i
+                // (0, 1 or 2: Frame.hpp's mask adds the two tone ranges),
+                // two bits each, built once per scan
+                int mbits = 0;
+                {
+                    const int tm = t0 & (T - 1);
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const int k = tm + T * i;
+                        mbits |= ((k >= a.a1 && k <= a.b1) + (k >= a.a2 && k <= a.b2)) << (2 * i);
+                    }
+                }
                 for (long base = pos;; base += 2L * G * N) {
                     if (const int ss = scan_stop(base)) {
                         stop = ss == 1;
@@ -2470,7 +2515,7 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
                     const long bA = base + (long)g * N, bB = bA + (long)G * N;
                     const bool liveA = ring ? (bA + N <= rend && bA < a.n) : bA + N <= a.n;
                     const bool liveB = ring ? (bB + N <= rend && bB < a.n) : bB + N <= a.n;
-                    float4 v[8];
+                    PCx v[8];
                     {
                         float2 va[8], vb[8];
                         if (ring && ((liveA && (bA < 0 || bA + N > a.n)) || (liveB && (bB < 0 || bB + N > a.n)))) {
@@ -2488,29 +2533,22 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
                             load8_block32<T, F>(a, bB + tt, liveB, vb);
                         }
 #pragma unroll
-                        for (int i = 0; i < 8; ++i) v[i] = make_float4(va[i].x, va[i].y, vb[i].x, vb[i].y);
+                        for (int i = 0; i < 8; ++i) v[i] = PCx{pf2{va[i].x, vb[i].x}, pf2{va[i].y, vb[i].y}};
                     }
-                    fft_regs_wave32x2<LOGT, -1>(v, tt, lds_tw, fftb32 + g * N);
-                    float ta = 0.f, sa = 0.f, tb = 0.f, sb = 0.f;
+                    fft_regs_wave32p<LOGT, -1>(v, tt, lds_tw, fftb32 + g * N);
+                    // per block: total energy and detector-bin energy (packed A | B)
+                    pf2 tot2 = {0.f, 0.f}, sin2 = {0.f, 0.f};
+                    int mb;
+                    asm volatile("v_mov_b32 %0, %1" : "=v"(mb) : "v"(mbits));
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {
-                        const int k = tt + T * i;
-                        const float m = (float)((k >= a.a1 && k <= a.b1) + (k >= a.a2 && k <= a.b2));
-                        const float ea = v[i].x * v[i].x + v[i].y * v[i].y;
-                        const float eb = v[i].z * v[i].z + v[i].w * v[i].w;
-                        ta += ea;
-                        sa += m * ea;
-                        tb += eb;
-                        sb += m * eb;
+                        const float m = (float)((mb >> (2 * i)) & 3);
+                        const pf2 e = v[i].re * v[i].re + v[i].im * v[i].im;
+                        tot2 += e;
+                        sin2 += pf2{m, m} * e;
                     }
-                    constexpr int W0 = T / 2;
-#pragma unroll
-                    for (int o = W0; o > 0; o >>= 1) {
-                        ta += __shfl_xor(ta, o);
-                        sa += __shfl_xor(sa, o);
-                        tb += __shfl_xor(tb, o);
-                        sb += __shfl_xor(sb, o);
-                    }
+                    const float ta = group_sum<T>(tot2.x), sa = group_sum<T>(sin2.x);
+                    const float tb = group_sum<T>(tot2.y), sb = group_sum<T>(sin2.y);
                     // 0 = certain FAIL, 1 = certain PASS, 2 = uncertain
                     auto screen = [&](bool live, float tot, float sine) -> int {
                         if (!live) return 0;
@@ -2945,7 +2983,7 @@ __global__ void __launch_bounds__(1024) resolve_kernel(ResolveArgs a)
         const bool ovf = nr[u] > MR;
         // an overflowed walk joins nothing; as c + 1 it hides no later anchor
         nxt[c] = ovf ? c + 1 : (lm[u] >= 0 ? lm[u] : C);
-        jx[c] = lj[u];
+        jx[c] = (lm[u] >= 0 && !ovf) ? lj[u] : 0;  // the link's entry index only where it joined
         onc[c] = 0;
         int e = (lm[u] >= 0 && !ovf) ? li[u] : min(nr[u], MR), bt = 0;
         const long* rc = a.rec + (long)c * MR;
@@ -3029,7 +3067,7 @@ __global__ void __launch_bounds__(1024) resolve_kernel(ResolveArgs a)
         if (u < CPT && c < C && onc[c]) {
             const int se = sege[c], e = se & 0xffff, bt = (se >> 16) & 0x3fff;
             if (se & SEG_OVF) atomicOr(&sflags, RESOLVE_OVERFLOW);  // its records are incomplete
-            const int b0 = ent[c], b = c == 0 ? max(b0, sfront) : b0;
+            const int b0 = min(ent[c], e), b = c == 0 ? max(b0, sfront) : b0;
             cnt[u] = max(0, e - b);
             fi[u] = b;
             chn += max(0, e + bt - b0);
@@ -3085,9 +3123,13 @@ __global__ void __launch_bounds__(1024) resolve_kernel(ResolveArgs a)
         oo += cnt[u];
     }
     __syncthreads();
+    // An overflowed chain chunk's records are incomplete: no list and a zero
+    // count, so the decode enqueued behind this kernel (the host has not read
+    // the flags yet) does nothing, and the host's halo walk writes every output
+    const bool overflow = (sflags & RESOLVE_OVERFLOW) != 0;  // uniform (set before the scan's barrier)
     // 5. owned slots, spread over the workgroups: slot -> its chunk by binary
     // search over the scan (last chunk with scan <= slot), then the record
-    const long lim = min(tot_own, a.cap);
+    const long lim = overflow ? 0 : min(tot_own, a.cap);
     for (long i0 = (long)blockIdx.x * NT * G; i0 < lim; i0 += (long)gridDim.x * NT * G) {
         long pbv[G];
 #pragma unroll
@@ -3118,7 +3160,7 @@ __global__ void __launch_bounds__(1024) resolve_kernel(ResolveArgs a)
         // the walkers' publication counts and chunk counter, zero for the next call
         for (int c = t; c < C; c += NT) a.pub[c] = 0;
         if (t == 0) {
-            *a.count = tot_own;
+            *a.count = overflow ? 0 : tot_own;
             if (a.queue_reset) *a.queue_reset = 0;
             // page-locked status the host polls: the fields, a system-scope
             // release, then the flags word it waits on (-1 until then)

@@ -58,7 +58,8 @@ class WalkTuning(C.Structure):
     """ofdm_walk_tuning: per-context stream walker settings (tests, experiments)."""
     _fields_ = [("chunks_per_slot", C.c_long), ("halo_milli", C.c_long), ("ext_milli", C.c_long),
                 ("exact_search", C.c_int), ("t2_f32", C.c_int), ("t2_margin", C.c_double),
-                ("allow_uncertified", C.c_int), ("staged_decode", C.c_int), ("lookback", C.c_int)]
+                ("allow_uncertified", C.c_int), ("staged_decode", C.c_int), ("lookback", C.c_int),
+                ("max_rec_cap", C.c_int)]
 
 
 class WalkState(C.Structure):
@@ -122,6 +123,8 @@ SIGNATURES = {
     "ofdm_stream_initial_state": (_I, [_V, C.POINTER(WalkState)]),
     "ofdm_set_stream_ring": (_I, [_V, _L]),
     "ofdm_get_stream_ring": (_I, [_V, C.POINTER(_L)]),
+    "ofdm_set_stream_timing": (_I, [_V, _I]),
+    "ofdm_get_stream_timing": (_I, [_V, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     "ofdm_stream_shard_margins": (_I, [_V, C.POINTER(_L), C.POINTER(_L)]),
     "ofdm_host_alloc": (_I, [_V, _SZ, C.POINTER(_V)]),
     "ofdm_host_free": (_I, [_V, _V]),
@@ -398,6 +401,17 @@ class Modem:
         if ring is not None:
             check(lib().ofdm_set_stream_ring(self.h, ring))
         return old.value
+
+    def stream_timing(self, on: bool) -> None:
+        """ofdm_set_stream_timing: per-phase HIP events in later stream calls."""
+        check(lib().ofdm_set_stream_timing(self.h, 1 if on else 0))
+
+    def last_stream_times(self) -> dict:
+        """ofdm_get_stream_timing: the last timed stream call's device times
+        (ms) of its walk, resolve and decode."""
+        w, r, d = C.c_float(), C.c_float(), C.c_float()
+        check(lib().ofdm_get_stream_timing(self.h, C.byref(w), C.byref(r), C.byref(d)))
+        return {"walk_ms": w.value, "resolve_ms": r.value, "decode_ms": d.value}
 
     def initial_state(self) -> tuple[int, int]:
         """ofdm_stream_initial_state: rx.cpp's first walk state (pos, ring_end)."""

@@ -209,7 +209,15 @@ class ShardedStreamRx:
         self.n_owned = n_own
         return self._report(loc, lag, ex, True)
 
+    def _check_cap(self, walk) -> None:
+        # the library's head/tail truncation of the located list and
+        # pack_report's windows must be the same frames: one cap sets both
+        wc = getattr(walk, "report_cap", self.cap)
+        if wc != self.cap:
+            raise ValueError(f"walker report_cap {wc} != ShardedStreamRx.cap {self.cap}")
+
     def first_walk(self, walk) -> ShardReport:
+        self._check_cap(walk)
         n_own, loc, lag, ex = walk(self._rel(self.speculative_start()))
         self.n_owned = n_own
         return self._report(loc, lag, ex, self.rank == 0)
@@ -294,7 +302,9 @@ def hip_walker(modem, x_slice, n_slice: int, own_lo_rel: int, own_hi_rel: int, m
     ofdm_rx_stream_shard; outputs: pb_out / bytes_out / constell_out / cfo_out
     device tensors for max_frames frames (pb relative to the slice). The
     located list holds the walk's first and last report_cap frames (all a
-    report packs, pack_report); walk.no_report(start_rel) skips it (one rank)."""
+    report packs, pack_report): pass the ShardedStreamRx's cap (its runs
+    refuse a walker whose report_cap differs); walk.no_report(start_rel)
+    skips the list (one rank)."""
     def walk(start_rel):
         return modem.rx_stream_shard(x_slice, n_slice, start_rel, own_lo_rel, own_hi_rel, max_frames,
                                      chunk=chunk, i16=i16, located_cap=2 * report_cap, stream=stream, **outputs)
@@ -303,4 +313,5 @@ def hip_walker(modem, x_slice, n_slice: int, own_lo_rel: int, own_hi_rel: int, m
         return modem.rx_stream_shard(x_slice, n_slice, start_rel, own_lo_rel, own_hi_rel, max_frames,
                                      chunk=chunk, i16=i16, located_cap=0, stream=stream, **outputs)[0]
     walk.no_report = no_report
+    walk.report_cap = report_cap
     return walk

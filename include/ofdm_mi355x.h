@@ -379,6 +379,16 @@ int ofdm_rx_stream_i16(ofdm_ctx* ctx, const int16_t* iq16, size_t n, size_t max_
 int ofdm_set_stream_ring(ofdm_ctx* ctx, long ring);
 int ofdm_get_stream_ring(const ofdm_ctx* ctx, long* ring);
 
+/* Measurement (no reference counterpart): with on = 1, every later stream
+ * call records HIP events around its walk, its resolve and its decode on the
+ * call's stream, and ofdm_get_stream_timing returns the last call's three
+ * device times in ms (waiting for its decode). The events sit between
+ * dependent kernels and cost launch gaps, so time the calls themselves with
+ * timing off. Fails when the last call had no timed decode (timing off, the
+ * halo walk, or a decode that is not the speculative one). */
+int ofdm_set_stream_timing(ofdm_ctx* ctx, int on);
+int ofdm_get_stream_timing(ofdm_ctx* ctx, float* walk_ms, float* resolve_ms, float* decode_ms);
+
 /* A state of the stream walk: the position of the next T2 search and, in
  * ring mode, one past the last sample of the ring buffer's current SDR
  * refill (stream coordinates; 0 without a ring). */
@@ -492,6 +502,9 @@ typedef struct ofdm_walk_tuning {
                              params -> rx kernels even where a fused decode
                              kernel fits (A/B measurements, tests; default 0) */
     int lookback;         /* 1: device-side look-back stitching (default 1)     */
+    int max_rec_cap;      /* test only: > 0 caps the records per walker (forces
+                             the look-back overflow and its halo-walk fallback;
+                             default 0 = the computed bound)                    */
 } ofdm_walk_tuning;
 int ofdm_walk_tuning_default(ofdm_walk_tuning* out);
 int ofdm_get_walk_tuning(const ofdm_ctx* ctx, ofdm_walk_tuning* out);

@@ -214,6 +214,30 @@ def test_stream_lookback_chain_across_chunks(nf, chunk, halo, ring):
     check_against_oracle(D, x, got, ring=ring)
 
 
+@pytest.mark.parametrize("ring", [None, 0], ids=["ring", "continuous"])
+@pytest.mark.parametrize("cap,chunk", [(1, 9000), (2, 20000), (1, 20000)])
+def test_stream_lookback_overflow_falls_back_to_halo_walk(cap, chunk, ring, monkeypatch, capfd):
+    """A look-back walker whose records overflow (the test hook max_rec_cap
+    shrinks its record buffer) makes the resolve kernel flag RESOLVE_OVERFLOW,
+    write no list and a zero count (the speculative decode behind it then
+    does nothing), and the host re-runs the call as the halo walk: every
+    output equals the oracle's and the host-stitched run's. The next call
+    with the normal bound runs on the same (now stale) walk scratch."""
+    x, data = impaired_stream(D, 40, seed=5, gap_max=6000)
+    monkeypatch.setenv("OFDM_STREAM_DEBUG", "1")
+    got = run_stream(D, x, chunk=chunk, ring=ring, tuning=dict(max_rec_cap=cap))
+    assert "look-back overflow" in capfd.readouterr().err  # the fallback branch ran
+    check_against_oracle(D, x, got, ring=ring)
+    halo = run_stream(D, x, chunk=chunk, ring=ring, tuning=dict(lookback=0))
+    assert got[0] == halo[0]
+    for a, b in zip(got[1:], halo[1:]):
+        assert np.array_equal(a, b)
+    again = run_stream(D, x, chunk=chunk, ring=ring)
+    assert "look-back overflow" not in capfd.readouterr().err
+    for a, b in zip(got, again):
+        assert np.array_equal(a, b)
+
+
 def test_stream_walk_certified_search_equals_serial_recurrence():
     # the walker's parallel preamble search (window sums + error bound) against
     # the reference's serial running-energy recurrence (ofdm_walk_tuning)
@@ -537,6 +561,9 @@ def test_walk_tuning_defaults_and_validation():
     assert t.staged_decode == 0
     with pytest.raises(M.OfdmError):
         m.walk_tuning(staged_decode=2)
+    assert t.max_rec_cap == 0
+    with pytest.raises(M.OfdmError):
+        m.walk_tuning(max_rec_cap=-1)
     m.walk_tuning()  # back to the defaults
 
 

@@ -37,7 +37,7 @@ def run_sharded(cfg, x, n, world, halo=None, i16=False, max_frames=None):
              "constell_out": torch.zeros((cap * g["npts"],), dtype=torch.complex128, device="cuda"),
              "cfo_out": torch.zeros((cap,), dtype=torch.float64, device="cuda")}
         walks.append(SS.hip_walker(m, xs, rx.slice_hi - rx.slice_lo, rx.own_lo - rx.slice_lo,
-                                   rx.own_hi - rx.slice_lo, cap, o, i16=i16))
+                                   rx.own_hi - rx.slice_lo, cap, o, i16=i16, report_cap=rx.cap))
         rxs.append(rx)
         outs.append((o, cap))
         mods.append(m)

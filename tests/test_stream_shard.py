@@ -205,3 +205,17 @@ def test_gloo_two_ranks_sharded_ring_walk_equals_sequential_walk():
         assert p.exitcode == 0
     owned = np.concatenate([np.array(o, np.int64) for _, o, _ in sorted(parts, key=lambda t: t[0])])
     assert np.array_equal(owned, want)
+
+
+def test_walker_report_cap_must_match_the_receiver_cap():
+    # the library truncates the located list to the walk's first and last
+    # report_cap frames, pack_report to the receiver's cap: one value for both
+    rx = S.ShardedStreamRx(D, 100000, 2, 1, cap=64)
+
+    def walk(start_rel):
+        return 0, [], [], (-1, 0)
+    walk.report_cap = 32
+    with pytest.raises(ValueError, match="report_cap"):
+        rx.first_walk(walk)
+    walk.report_cap = 64
+    rx.first_walk(walk)
