@@ -423,6 +423,65 @@ def stream_pipelined(args, p, M, dev, modem, layout, rx, walk, outs, x, nsl, cap
                     "overlaps call k's decode); the record's value is the serial per-call figure"}
 
 
+def stream_ingest_leg(args, dev, M):
+    """A stream that keeps arriving (rx.cpp:58-91: the SDR reader thread and
+    buf[2]): the config-4 int16 wire stream in page-locked host memory,
+    received chunk by chunk (ofdm_ingest.StreamIngest: H2D of chunk k+1 on a
+    copy stream while chunk k walks and decodes; each chunk's walk starts
+    from the previous one's exit state). value = stream samples / s end to
+    end (first copy to last decode), against the PCIe ceiling measured here
+    (one pinned H2D copy of the whole stream); outputs compared with one
+    device-resident call over the same stream. One GPU."""
+    import torch
+    import ofdm_ingest as I
+    import ofdm_synth as Y
+    p = dict(CONFIG_D)
+    modem = M.Modem(p, dev.index)
+    layout = Y.StreamLayout(p, args.stream_frames)
+    x16 = Y.stream_slice(modem, layout, 0, layout.n, dev, i16=True)
+    host = I.host_pinned_i16(x16)
+    cap = layout.total_frames + 16
+    npts = p["num_data_subc"] * p["num_symb"]
+
+    def outs():
+        return {"pb_out": torch.full((cap,), -1, dtype=torch.int64, device=dev),
+                "bytes_out": torch.zeros((cap * layout.bpf,), dtype=torch.uint8, device=dev),
+                "constell_out": torch.zeros((cap * npts,), dtype=torch.complex128, device=dev),
+                "cfo_out": torch.zeros((cap,), dtype=torch.float64, device=dev)}
+    ref = outs()
+    nref = modem.rx_stream_i16(x16, layout.n, cap, **ref)
+    got = outs()
+    ing = I.StreamIngest(modem, p, host, layout.n, args.ingest_chunk, got, dev, cap)
+    ing.run()  # warm-up (buffers, kernels)
+    torch.cuda.synchronize(dev)
+    reps = max(1, args.ingest_reps)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        res = ing.run()
+    torch.cuda.synchronize(dev)
+    el = (time.perf_counter() - t0) / reps
+    same = res["frames"] == nref and all(bool(torch.equal(got[k], ref[k])) for k in got)
+    # the PCIe ceiling: one page-locked H2D copy of the whole stream
+    d = torch.empty_like(x16)
+    d.copy_(host, non_blocking=True)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    d.copy_(host, non_blocking=True)
+    torch.cuda.synchronize(dev)
+    h2d_s = time.perf_counter() - t1
+    del d
+    modem.close()
+    return {"metric": "stream samples/s end to end from host memory (int16 wire samples H2D overlapped with "
+                      "walk + decode)", "workload": STREAM_WORKLOAD + "_int16_host_ingest",
+            "value": layout.n / el, "unit": "stream samples/s", "n_gpus": 1, "reps": reps,
+            "ms_per_stream": el * 1e3, "chunk_samples": args.ingest_chunk, "calls_per_stream": res["calls"],
+            "stream_samples": layout.n, "frames_found": res["frames"],
+            "outputs_equal_device_resident_call": same,
+            "pcie_h2d": {"GB_per_s": layout.n * 4 / h2d_s / 1e9, "samples_per_s": layout.n / h2d_s,
+                         "note": "one page-locked H2D copy of the whole int16 stream, measured in this run"},
+            "frac_of_pcie_ceiling": (layout.n / el) / (layout.n / h2d_s)}
+
+
 CONFIG_C = dict(CONFIG_B, fft_size=4096, num_data_subc=2048, num_pilot_subc=64, cp_size=1024, mod_type=4)
 
 
@@ -532,8 +591,12 @@ def main():
     ap.add_argument("--stream-cpu-budget", type=float, default=8.0)
     ap.add_argument("--stream-b-frames", type=int, default=4096,
                     help="config-B stream frames per GPU for the stream_B sub-record (0: skip)")
-    ap.add_argument("--stream-pipeline", type=int, default=2,
-                    help="contexts for the stream record's pipelined figure (1: off; one GPU only)")
+    ap.add_argument("--stream-pipeline", type=int, default=1,
+                    help="contexts for the stream record's two-context figure (1: off, the default: one context "
+                         "per GPU is the supported mode, INTEGRATION.md; one GPU only)")
+    ap.add_argument("--no-ingest", action="store_true", help="skip the host-ingest stream sub-record")
+    ap.add_argument("--ingest-chunk", type=int, default=1 << 22, help="stream samples per ingest call")
+    ap.add_argument("--ingest-reps", type=int, default=3)
     ap.add_argument("--no-config3", action="store_true", help="skip the config-3 (config C) sub-record")
     ap.add_argument("--config3-frames", type=int, default=4096, help="config C frames per GPU (weak)")
     ap.add_argument("--config3-warmup", type=int, default=30, help="untimed config-3 steps (clock ramp)")
@@ -620,6 +683,8 @@ def main():
             record("stream_B", lambda: stream_leg(args, dist, dev, world, rank, M, i16=False, p=CONFIG_B,
                                                   frames_per_gpu=args.stream_b_frames, workload=STREAM_WORKLOAD_B,
                                                   pipeline=False, staged_ab=True, deferred=deferred))
+        if not args.no_ingest and world == 1:  # host ingest: one GPU's PCIe link
+            record("stream_ingest", lambda: stream_ingest_leg(args, dev, M))
     if not args.no_config3:
         record("config3", lambda: config3_leg(args, dist, dev, world, rank, M))
 

@@ -13,6 +13,22 @@
 //                 [--snr-db X] [--plan-only]
 //   --plan-only prints each rank's frame range and a stream's shard plan and
 //   touches no GPU.
+//
+// Stream mode (BASELINE configs[3] over N GPUs; the reference's
+// receive loop rx.cpp:125-221 sharded by samples):
+//   ofdm_multigpu --stream FILE [--f64] [--config CFG] [--shards N] [--gpus G]
+//                 [--report-cap C] [--reps K] [--pbs-out FILE]
+//   FILE holds the stream as the SDR delivers it, complex<int16> pairs (or
+//   complex<double> with --f64). N ranks (default: one per GPU), rank r on
+//   device r % G, each with its own ofdm_ctx and thread: it walks and decodes
+//   its slice (ofdm_stream_shard_plan, ofdm_rx_stream_shard), packs its
+//   report row (ofdm_stream_report_pack), the ranks all-gather the rows
+//   (ncclAllGather with one rank per GPU; through host memory when ranks
+//   share a GPU, the in-process mode) and all run the same plan
+//   (ofdm_stream_stitch_plan): the rank it names re-walks from its
+//   predecessor's exit state, and the exchange repeats until every walk is
+//   accepted. Prints one JSON line; --pbs-out writes every owned frame's
+//   preamble start (int64, stream order): the sequential walk's frames.
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -91,12 +107,20 @@ struct Barrier {  // the ranks' host barrier (threads of this process)
 
 }  // namespace
 
+// the stream mode (see the header comment); returns the process exit code
+int stream_main(const std::string& path, bool f64, const std::string& cfg, int shards, int gpus, size_t cap,
+                int reps, const std::string& pbs_out);
+
 int main(int argc, char** argv)
 {
     int gpus = 0, steps = 20, warmup = 5;
     long frames = 8192, total_frames = 0;
     double snr_db = 10.0;
     bool plan_only = false;
+    std::string stream_path, cfg_path, pbs_out;
+    bool f64 = false;
+    int shards = 0, reps = 1;
+    size_t cap = 64;
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
         auto next = [&]() { return i + 1 < argc ? argv[++i] : (std::fprintf(stderr, "%s needs a value\n", a.c_str()), std::exit(2), ""); };
@@ -107,12 +131,21 @@ int main(int argc, char** argv)
         else if (a == "--warmup") warmup = std::atoi(next());
         else if (a == "--snr-db") snr_db = std::atof(next());
         else if (a == "--plan-only") plan_only = true;
+        else if (a == "--stream") stream_path = next();
+        else if (a == "--f64") f64 = true;
+        else if (a == "--config") cfg_path = next();
+        else if (a == "--shards") shards = std::atoi(next());
+        else if (a == "--report-cap") cap = (size_t)std::atol(next());
+        else if (a == "--reps") reps = std::atoi(next());
+        else if (a == "--pbs-out") pbs_out = next();
         else {
             std::fprintf(stderr, "usage: %s [--gpus N] [--frames F | --total-frames T] [--steps K] [--warmup W] "
-                                 "[--snr-db X] [--plan-only]\n", argv[0]);
+                                 "[--snr-db X] [--plan-only] | --stream FILE [--f64] [--config CFG] [--shards N] "
+                                 "[--gpus G] [--report-cap C] [--reps K] [--pbs-out FILE]\n", argv[0]);
             return 2;
         }
     }
+    if (!stream_path.empty()) return stream_main(stream_path, f64, cfg_path, shards, gpus, cap, reps, pbs_out);
     const ofdm_params p = config_b();
     const long L = p.fft_size + p.cp_size, msg = L * p.num_symb;
     const long bpf = p.num_data_subc * p.num_symb * p.mod_type / 8;
@@ -208,5 +241,199 @@ int main(int argc, char** argv)
                 totals[2] / el, gpus, steps, warmup, el / steps * 1e3, total_frames > 0 ? "strong" : "weak",
                 (long long)totals[0], (long long)totals[1], totals[1] ? (double)totals[0] / totals[1] : 0.0,
                 (long long)totals[3]);
+    return 0;
+}
+
+// ---------------------------------------------------------------- stream mode
+namespace {
+
+struct RankRx {  // one rank's context, slice and outputs
+    ofdm_ctx* c = nullptr;
+    void* st = nullptr;
+    long slice_lo = 0, slice_hi = 0, own_lo = 0, own_hi = 0;
+    void *d_iq = nullptr, *d_pb = nullptr, *d_bytes = nullptr, *d_cons = nullptr, *d_cfo = nullptr;
+    size_t max_frames = 0, n_owned = 0;
+    int rewalks = 0;
+    std::vector<long> located;
+    std::vector<uint8_t> lag;
+    std::vector<int64_t> row;
+};
+
+}  // namespace
+
+int stream_main(const std::string& path, bool f64, const std::string& cfg, int shards, int gpus, size_t cap,
+                int reps, const std::string& pbs_out)
+{
+    ofdm_params p{};
+    if (cfg.empty() ? ofdm_params_default(&p) : ofdm_params_from_config(cfg.c_str(), &p)) die(0, "config");
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) {
+        std::fprintf(stderr, "cannot open %s\n", path.c_str());
+        return 1;
+    }
+    std::fseek(f, 0, SEEK_END);
+    const long bytes = std::ftell(f);
+    std::fseek(f, 0, SEEK_SET);
+    const size_t esz = f64 ? 16 : 4;
+    const size_t n = (size_t)bytes / esz;
+    std::vector<char> host((size_t)bytes);
+    if (std::fread(host.data(), 1, host.size(), f) != host.size()) {
+        std::fprintf(stderr, "short read %s\n", path.c_str());
+        return 1;
+    }
+    std::fclose(f);
+    int ndev = 0;
+    if (ofdm_device_count(&ndev) != OFDM_OK || ndev < 1) die(0, "ofdm_device_count");
+    if (gpus <= 0 || gpus > ndev) gpus = ndev;
+    const int world = shards > 0 ? shards : gpus;
+    // one rank per GPU: RCCL moves the rows; ranks sharing a GPU: host memory
+    const bool rccl = world == gpus && world > 1;
+    std::vector<ncclComm_t> comms;
+    if (rccl) {
+        comms.resize(world);
+        std::vector<int> devs(world);
+        for (int r = 0; r < world; ++r) devs[r] = r;
+        if (ncclCommInitAll(comms.data(), world, devs.data()) != ncclSuccess) {
+            std::fprintf(stderr, "ncclCommInitAll failed\n");
+            return 1;
+        }
+    }
+    const size_t len = OFDM_STREAM_REPORT_HEADER + 2 * cap;
+    const long L = p.fft_size + p.cp_size, flen = p.t2sin_size + L * (p.num_pr_symb + p.num_symb);
+    const long bpf = p.num_data_subc * p.num_symb * p.mod_type / 8, npts = (long)p.num_data_subc * p.num_symb;
+    std::vector<RankRx> rk(world);
+    std::vector<int64_t> rows(world * len);  // the all-gathered rows (every rank reads them)
+    Barrier bar(world);
+    std::vector<double> elapsed(world, 0.0);
+    std::vector<int> plan_rank(1, -1);
+    std::vector<ofdm_walk_state> plan_start(1);
+    std::vector<std::vector<long>> owned(world);
+
+    auto rank_main = [&](int r) {
+        RankRx& x = rk[r];
+        CHECK(r, ofdm_create(&p, r % gpus, &x.c));
+        CHECK(r, ofdm_stream_create(x.c, &x.st));
+        CHECK(r, ofdm_stream_shard_plan(&p, n, world, r, &x.slice_lo, &x.slice_hi, &x.own_lo, &x.own_hi));
+        const size_t ns = (size_t)(x.slice_hi - x.slice_lo);
+        x.max_frames = ns / (size_t)flen + 16;
+        CHECK(r, ofdm_device_alloc(x.c, std::max<size_t>(1, ns * esz), &x.d_iq));
+        CHECK(r, ofdm_device_alloc(x.c, x.max_frames * sizeof(long), &x.d_pb));
+        CHECK(r, ofdm_device_alloc(x.c, x.max_frames * bpf, &x.d_bytes));
+        CHECK(r, ofdm_device_alloc(x.c, x.max_frames * npts * 16, &x.d_cons));
+        CHECK(r, ofdm_device_alloc(x.c, x.max_frames * sizeof(double), &x.d_cfo));
+        CHECK(r, ofdm_memcpy_h2d(x.c, x.d_iq, host.data() + (size_t)x.slice_lo * esz, ns * esz, x.st));
+        long ring = 0;
+        CHECK(r, ofdm_get_stream_ring(x.c, &ring));
+        x.located.resize(2 * cap);
+        x.lag.resize(2 * cap);
+        x.row.resize(len);
+        void *d_row = nullptr, *d_rows = nullptr;
+        if (rccl) {
+            CHECK(r, ofdm_device_alloc(x.c, len * sizeof(int64_t), &d_row));
+            CHECK(r, ofdm_device_alloc(x.c, world * len * sizeof(int64_t), &d_rows));
+        }
+        // walk from an absolute state, pack the report row
+        auto walk = [&](ofdm_walk_state s, bool true_start) {
+            ofdm_walk_state rel{s.pos - x.slice_lo, ring ? s.ring_end - x.slice_lo : 0}, ex{};
+            size_t nl = 0, nf = 0;
+            if (s.pos < 0 && r > 0) {  // the true walk ended before this core: nothing owned
+                x.n_owned = 0;
+                nl = 0;
+                ex = ofdm_walk_state{-1, 0};
+            } else {
+                CHECK(r, ofdm_rx_stream_shard(x.c, f64 ? (const double*)x.d_iq : nullptr,
+                                              f64 ? nullptr : (const int16_t*)x.d_iq, ns, &rel, x.own_lo - x.slice_lo,
+                                              x.own_hi - x.slice_lo, x.max_frames, 0, (long*)x.d_pb,
+                                              (uint8_t*)x.d_bytes, (double*)x.d_cons, (double*)x.d_cfo, &nf,
+                                              x.located.data(), x.lag.data(), 2 * cap, &nl, &ex, x.st));
+                x.n_owned = std::min(nf, x.max_frames);
+                if (ex.pos >= 0) ex = ofdm_walk_state{ex.pos + x.slice_lo, ring ? ex.ring_end + x.slice_lo : 0};
+            }
+            const size_t k = std::min(nl, 2 * cap);
+            for (size_t i = 0; i < k; ++i) x.located[i] += x.slice_lo;
+            CHECK(r, ofdm_stream_report_pack(r, x.slice_lo, x.own_lo, x.own_hi, x.located.data(), x.lag.data(), k,
+                                             &ex, true_start ? 1 : 0, cap, x.row.data()));
+        };
+        auto exchange = [&]() {
+            if (rccl) {
+                CHECK(r, ofdm_memcpy_h2d(x.c, d_row, x.row.data(), len * sizeof(int64_t), x.st));
+                if (ncclAllGather(d_row, d_rows, len, ncclInt64, comms[r], (hipStream_t)x.st) != ncclSuccess)
+                    die(r, "ncclAllGather");
+                std::vector<int64_t> all(world * len);
+                CHECK(r, ofdm_memcpy_d2h(x.c, all.data(), d_rows, all.size() * sizeof(int64_t), x.st));
+                CHECK(r, ofdm_stream_synchronize(x.c, x.st));
+                bar.wait();
+                if (r == 0) rows = all;
+                bar.wait();
+            } else {
+                bar.wait();  // every rank's row is final
+                std::copy(x.row.begin(), x.row.end(), rows.begin() + r * len);
+                bar.wait();
+            }
+        };
+        for (int it = 0; it < reps; ++it) {
+            bar.wait();
+            const auto t0 = std::chrono::steady_clock::now();
+            ofdm_walk_state s0{};
+            if (r == 0) {
+                CHECK(r, ofdm_stream_initial_state(x.c, &s0));
+            } else {
+                s0 = ofdm_walk_state{x.slice_lo, ring ? (x.slice_lo / ring + 1) * ring : 0};
+            }
+            walk(s0, r == 0);
+            x.rewalks = 0;
+            for (;;) {
+                exchange();
+                if (r == 0) CHECK(r, ofdm_stream_stitch_plan(rows.data(), world, cap, p.t2sin_size, &plan_rank[0],
+                                                             &plan_start[0]));
+                bar.wait();
+                const int pr = plan_rank[0];
+                const ofdm_walk_state ps = plan_start[0];
+                bar.wait();  // every rank has read the plan
+                if (pr < 0) break;
+                if (pr == r) {
+                    walk(ps, true);
+                    ++x.rewalks;
+                }
+            }
+            CHECK(r, ofdm_stream_synchronize(x.c, x.st));  // the decodes
+            bar.wait();
+            elapsed[r] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        }
+        std::vector<long> pb(x.n_owned);
+        if (x.n_owned) CHECK(r, ofdm_memcpy_d2h(x.c, pb.data(), x.d_pb, x.n_owned * sizeof(long), x.st));
+        CHECK(r, ofdm_stream_synchronize(x.c, x.st));
+        for (long& v : pb) v += x.slice_lo;
+        owned[r] = pb;
+        for (void* d : {x.d_iq, x.d_pb, x.d_bytes, x.d_cons, x.d_cfo, d_row, d_rows})
+            if (d) ofdm_device_free(x.c, d);
+        ofdm_stream_destroy(x.c, x.st);
+        ofdm_destroy(x.c);
+    };
+    std::vector<std::thread> th;
+    for (int r = 0; r < world; ++r) th.emplace_back(rank_main, r);
+    for (auto& t : th) t.join();
+    for (auto& cm : comms) ncclCommDestroy(cm);
+    size_t total = 0;
+    int rewalks = 0;
+    for (int r = 0; r < world; ++r) {
+        total += owned[r].size();
+        rewalks += rk[r].rewalks;
+    }
+    if (!pbs_out.empty()) {
+        FILE* o = std::fopen(pbs_out.c_str(), "wb");
+        if (!o) die(0, "pbs-out");
+        for (int r = 0; r < world; ++r)
+            if (!owned[r].empty()) std::fwrite(owned[r].data(), sizeof(long), owned[r].size(), o);
+        std::fclose(o);
+    }
+    const double el = *std::max_element(elapsed.begin(), elapsed.end());
+    std::printf("{\"metric\": \"stream samples/s (T2 walk + preamble sync + CFO/CP/phase/chan sync + demod), "
+                "sharded stream\", \"value\": %.6e, \"unit\": \"stream samples/s\", \"ranks\": %d, \"gpus\": %d, "
+                "\"exchange\": \"%s\", \"stream_samples\": %zu, \"format\": \"%s\", \"frames\": %zu, "
+                "\"rewalks\": %d, \"ms_per_stream\": %.4f, \"host\": \"C++ over the C-ABI, one thread + ofdm_ctx per "
+                "rank, report rows all-gathered, ofdm_stream_stitch_plan\"}\n",
+                n / el, world, gpus, rccl ? "ncclAllGather" : "host memory (ranks share a GPU)", n,
+                f64 ? "complex<double>" : "complex<int16>", total, rewalks, el * 1e3);
     return 0;
 }

@@ -17,6 +17,7 @@
 #include <mutex>
 #include <cstring>
 #include <fstream>
+#include <iterator>
 #include <random>
 #include <stdexcept>
 #include <string>
@@ -1398,10 +1399,15 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     const long R = c->ring, flen0 = c->geo.frame_len;
     const long start = start_state.pos;
     // ring mode: the walk may start in rx.cpp's zero header before the first
-    // SDR buffer ([-output_size, 0)); its ring end lies ahead of it, within R
-    if (R > 0 ? (start < -flen0 || start_state.ring_end <= start || start_state.ring_end > start + R + flen0)
+    // SDR buffer ([-output_size, 0)); its ring end lies ahead of it, within R.
+    // An exit state may also lie a little past its ring end: a walk that
+    // crossed own_hi inside a T2 scan whose next block leaves the ring (the
+    // state's next step is the refill, pos = ring_end, rx.cpp:137-145)
+    const long past = ofdm::WALK_SCAN_MAX + c->t2;
+    if (R > 0 ? (start < -flen0 || start_state.ring_end <= start - past || start_state.ring_end > start + R + flen0)
               : start < 0)
-        return fail(OFDM_ERR_INVALID, "start state out of range (ring mode: -output_size <= pos < ring_end <= pos + R + output_size)");
+        return fail(OFDM_ERR_INVALID, "start state out of range (ring mode: -output_size <= pos, pos - %ld < ring_end "
+                                      "<= pos + R + output_size)", past);
     if (own_lo < 0 || own_lo > own_hi || own_hi > (long)n)
         return fail(OFDM_ERR_INVALID, "need 0 <= own_lo <= own_hi <= n");
     if (c->t2_logn < 6 || c->t2_logn > 11) return fail(OFDM_ERR_UNSUPPORTED, "stream walk needs T2sin_size = 2^a, 64..2048");
@@ -2176,6 +2182,66 @@ int ofdm_reduce_counters(ofdm_ctx* c, int64_t* counters, size_t count, void* com
     HIP_TRY(hipSetDevice(c->device));
     const int r = all_reduce(counters, counters, count, kRcclInt64, kRcclSum, comm, (hipStream_t)stream);
     if (r != 0) return fail(OFDM_ERR_HIP, "ncclAllReduce: %s", err_str ? err_str(r) : "error");
+    return OFDM_OK;
+}
+
+int ofdm_stream_report_pack(int rank, long slice_lo, long own_lo, long own_hi, const long* located,
+                            const uint8_t* located_lag, size_t nlocated, const ofdm_walk_state* exit_state,
+                            int true_start, size_t cap, int64_t* row)
+{
+    // ofdm_stream.py pack_report: header, then the walk's first and last cap
+    // located frames, each as 2*pb + lag (-1: empty)
+    if (!row || !exit_state || (nlocated && !located) || cap < 1) return fail(OFDM_ERR_INVALID, "null argument or cap 0");
+    const size_t H = OFDM_STREAM_REPORT_HEADER;
+    const int64_t head[H] = {rank, slice_lo, own_lo, own_hi, exit_state->pos, exit_state->ring_end, true_start ? 1 : 0};
+    std::copy(head, head + H, row);
+    std::fill(row + H, row + H + 2 * cap, (int64_t)-1);
+    auto key = [&](size_t i) { return 2 * (int64_t)located[i] + (located_lag && located_lag[i] ? 1 : 0); };
+    const size_t nh = std::min(nlocated, cap);
+    for (size_t i = 0; i < nh; ++i) row[H + i] = key(i);
+    if (nlocated > cap)
+        for (size_t i = 0; i < cap; ++i) row[H + cap + i] = key(nlocated - cap + i);
+    return OFDM_OK;
+}
+
+int ofdm_stream_stitch_plan(const int64_t* rows, int world, size_t cap, long t2, int* rank_out,
+                            ofdm_walk_state* start_out)
+{
+    // ofdm_stream.py unpack_report + stitch_plan + rewalk_start
+    if (!rows || !rank_out || !start_out || world < 1 || cap < 1 || t2 < 1)
+        return fail(OFDM_ERR_INVALID, "need rows, outputs, world >= 1, cap >= 1, t2sin_size >= 1");
+    const size_t H = OFDM_STREAM_REPORT_HEADER, len = H + 2 * cap;
+    auto keys = [&](int r) {  // the rank's located keys (2*pb + lag), sorted, unique
+        std::vector<int64_t> k;
+        for (size_t i = H; i < len; ++i)
+            if (rows[r * len + i] >= 0) k.push_back(rows[r * len + i]);
+        std::sort(k.begin(), k.end());
+        k.erase(std::unique(k.begin(), k.end()), k.end());
+        return k;
+    };
+    *rank_out = -1;
+    *start_out = ofdm_walk_state{-1, 0};
+    for (int r = 1; r < world; ++r) {
+        const int64_t* cur = rows + r * len;
+        const int64_t* prev = rows + (r - 1) * len;
+        if (cur[6]) continue;  // walked from a true state
+        const std::vector<int64_t> kc = keys(r), kp = keys(r - 1);
+        int64_t first = INT64_MAX;  // the first owned frame's preamble start
+        for (int64_t k : kc)
+            if ((k >> 1) >= cur[2] && (k >> 1) < cur[3]) first = std::min(first, k >> 1);
+        std::vector<int64_t> common;
+        std::set_intersection(kc.begin(), kc.end(), kp.begin(), kp.end(), std::back_inserter(common));
+        bool ok = false;
+        for (int64_t k : common) ok = ok || (k >> 1) <= first;
+        if (ok) continue;
+        *rank_out = r;
+        if (prev[4] < 0) return OFDM_OK;  // the true walk ran out of samples before this core
+        long pos = (long)prev[4];
+        const long slice_lo = (long)cur[1];
+        if (pos < slice_lo) pos += (slice_lo - pos + t2 - 1) / t2 * t2;  // forward on its own T2 grid
+        *start_out = ofdm_walk_state{pos, (long)prev[5]};
+        return OFDM_OK;
+    }
     return OFDM_OK;
 }
 

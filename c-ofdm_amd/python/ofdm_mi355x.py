@@ -142,6 +142,8 @@ SIGNATURES = {
     "ofdm_stream_shard_plan": (_I, [_PP, _SZ, _I, _I, C.POINTER(_L), C.POINTER(_L), C.POINTER(_L), C.POINTER(_L)]),
     "ofdm_reduce_counters": (_I, [_V, _V, _SZ, _V, _V]),
     "ofdm_device_count": (_I, [C.POINTER(_I)]),
+    "ofdm_stream_report_pack": (_I, [_I, _L, _L, _L, _V, _V, _SZ, C.POINTER(WalkState), _I, _SZ, _V]),
+    "ofdm_stream_stitch_plan": (_I, [_V, _I, _SZ, _L, C.POINTER(_I), C.POINTER(WalkState)]),
 }
 
 _lib = None

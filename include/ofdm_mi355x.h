@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define OFDM_MI355X_ABI_VERSION 4
+#define OFDM_MI355X_ABI_VERSION 5
 
 enum {
     OFDM_OK = 0,
@@ -411,11 +411,14 @@ int ofdm_stream_initial_state(const ofdm_ctx* ctx, ofdm_walk_state* out);
  * also fixes the ring ends' phase: start->ring_end + k*R) and the frames
  * located with pb in [own_lo, own_hi) are decoded into the outputs exactly as
  * ofdm_rx_stream does (pb_out relative to iq). Requires 0 <= own_lo <= own_hi
- * <= n and start->pos >= 0 (ring mode: >= -output_size, start->pos <
- * start->ring_end <= start->pos + R + output_size).
+ * <= n and start->pos >= 0 (ring mode: >= -output_size, start->pos - 2048 -
+ * T2sin_size < start->ring_end <= start->pos + R + output_size).
  *   *exit_out: the walk's first state at or past own_hi (where the next
  *     shard's walk resumes; a state equivalent to it, or the state whose step
  *     located the first frame past own_hi), pos -1 if the samples ran out.
+ *     In ring mode its pos may lie up to one T2 scan step past its ring end
+ *     (a scan that crossed own_hi where the ring runs out: its next step is
+ *     the refill); it is a valid start state for the next call.
  *   located (host, nullable, located_cap entries) / located_lag (host,
  *     nullable: ring mode's state after the frame has the later of its two
  *     possible ring ends) / *nlocated_out (nullable): the frames the walk
@@ -466,6 +469,40 @@ int ofdm_stream_shard_plan(const ofdm_params* params, size_t n, int world, int r
 int ofdm_reduce_counters(ofdm_ctx* ctx, int64_t* counters, size_t count, void* nccl_comm, void* stream);
 /* Visible HIP devices (0 and OFDM_ERR_HIP without a GPU). */
 int ofdm_device_count(int* count);
+
+/* The sharded stream's report exchange (the protocol of
+ * c-ofdm_amd/python/ofdm_stream.py, which these restate for C/C++ hosts).
+ * Each rank walks its slice (ofdm_rx_stream_shard: rank 0 from the stream's
+ * initial state, the others speculatively from their slice start with the
+ * first ring end after it), packs a fixed-size report row, and the ranks
+ * all-gather the rows (one ncclAllGather of int64). Every rank then runs the
+ * same plan on the same rows: the first rank whose walk is not yet known to
+ * be the true walk re-walks from the state the plan returns (its
+ * predecessor's exit state), re-packs its row with true_start = 1, and the
+ * exchange repeats until the plan accepts every rank. The union of the owned
+ * frames is then exactly the one sequential walk's (rx.cpp:125-221).
+ * Row length in int64: OFDM_STREAM_REPORT_HEADER + 2 * cap. */
+#define OFDM_STREAM_REPORT_HEADER 7
+/* Pack a report row. located / located_lag: the walk's located frames in
+ * walk order (ABSOLUTE preamble starts: ofdm_rx_stream_shard's relative ones
+ * plus slice_lo) and their ring lags (NULL: all 0), nlocated of them, as
+ * ofdm_rx_stream_shard returns them with located_cap = 2 * cap (the walk's
+ * first and last cap frames when longer); exit_state absolute (pos -1: the
+ * samples ran out); true_start: the walk started from a state of the true
+ * walk (rank 0, or a re-walk). row: OFDM_STREAM_REPORT_HEADER + 2 * cap. */
+int ofdm_stream_report_pack(int rank, long slice_lo, long own_lo, long own_hi, const long* located,
+                            const uint8_t* located_lag, size_t nlocated, const ofdm_walk_state* exit_state,
+                            int true_start, size_t cap, int64_t* row);
+/* The plan over the world's rows (rank order, each packed with the same
+ * cap): *rank_out = the first rank to re-walk and *start_out the absolute
+ * state to re-walk it from (pos -1: the true walk ended before that rank's
+ * core, so it and the ranks after it own no frame), or *rank_out = -1 when
+ * every walk is accepted. Rank r is accepted when it was walked from a true
+ * state, or when it and rank r-1 located a common frame (same preamble start
+ * and lag) no later than r's first owned frame. t2sin_size: the config's
+ * (an exit state before the slice moves forward on its own T2 grid). */
+int ofdm_stream_stitch_plan(const int64_t* rows, int world, size_t cap, long t2sin_size, int* rank_out,
+                            ofdm_walk_state* start_out);
 
 /* ---- stream walk tuning (tests and experiments) --------------------------
  * Per-context settings of the ofdm_rx_stream* walkers; ofdm_create sets the

@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in declared if not hasattr(L, n)]
     assert missing == []
     assert set(declared) == set(M.SIGNATURES), "python binding out of sync with the header"
-    assert L.ofdm_abi_version() == 4
+    assert L.ofdm_abi_version() == 5
 
 
 def test_params_default_is_committed_config():
@@ -152,3 +152,52 @@ def test_multigpu_app_plan_only():
     assert d["world"] == 8 and len(d["ranks"]) == 8
     for r in d["ranks"]:
         assert (r["first"], r["count"]) == ofdm_dist.shard(30517, 8, r["rank"])
+
+
+def test_stream_report_pack_and_stitch_plan_match_python_protocol():
+    # the C-ABI's report row and stitch plan (ofdm_stream_report_pack /
+    # ofdm_stream_stitch_plan, for C/C++ hosts) against ofdm_stream.py's
+    # pack_report / unpack_report / stitch_plan on random reports: accepted
+    # ranks, re-walks from the predecessor's exit state (before the slice:
+    # moved forward on the T2 grid), walks that ran out, long located lists
+    import numpy as np
+    import ofdm_stream as SS
+    L = M.lib()
+    rng = np.random.default_rng(7)
+    t2 = 256
+    for trial in range(300):
+        world = int(rng.integers(1, 6))
+        cap = int(rng.integers(1, 9))
+        reps, rows_c = [], []
+        base = 0
+        for r in range(world):
+            own_lo = base
+            own_hi = own_lo + int(rng.integers(10000, 60000))
+            slice_lo = max(0, own_lo - int(rng.integers(0, 20000)))
+            base = own_hi
+            nloc = int(rng.integers(0, 3 * cap + 2))
+            pbs = np.sort(rng.choice(np.arange(slice_lo, own_hi + 8000, 97), size=nloc, replace=False))
+            if r > 0 and reps and reps[-1].located and rng.random() < 0.5:  # share a frame with the predecessor
+                shared = reps[-1].located[int(rng.integers(0, len(reps[-1].located)))][0]
+                pbs = np.sort(np.unique(np.append(pbs, shared)))
+            lags = rng.integers(0, 2, size=len(pbs)).astype(np.uint8)
+            ex = (-1, 0) if rng.random() < 0.1 else (int(own_hi - rng.integers(-3000, 6000)), int(rng.integers(0, 10**6)))
+            true_start = r == 0 or rng.random() < 0.2
+            rep = SS.ShardReport(r, slice_lo, own_lo, own_hi, [(int(p), int(g)) for p, g in zip(pbs, lags)], ex,
+                                 true_start)
+            reps.append(rep)
+            row_py = SS.pack_report(rep, cap)
+            row = np.empty(SS.HEADER + 2 * cap, dtype=np.int64)
+            la = np.ascontiguousarray(pbs, dtype=np.int64)
+            M.check(L.ofdm_stream_report_pack(r, slice_lo, own_lo, own_hi, la.ctypes.data, lags.ctypes.data, len(pbs),
+                                              C.byref(M.WalkState(*ex)), int(true_start), cap, row.ctypes.data))
+            assert np.array_equal(row, row_py), (trial, r)
+            rows_c.append(row)
+        plan_py = SS.stitch_plan([SS.unpack_report(rw, cap) for rw in rows_c], t2)
+        allr = np.ascontiguousarray(np.stack(rows_c))
+        rk, st = C.c_int(), M.WalkState()
+        M.check(L.ofdm_stream_stitch_plan(allr.ctypes.data, world, cap, t2, C.byref(rk), C.byref(st)))
+        if plan_py is None:
+            assert rk.value == -1
+        else:
+            assert (rk.value, (st.pos, st.ring_end)) == (plan_py[0], tuple(plan_py[1])), trial

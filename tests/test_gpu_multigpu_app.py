@@ -62,3 +62,51 @@ def test_multigpu_app_strong_scaling_shard():
     d = run_app("--gpus", "1", "--total-frames", "1001", "--steps", "2", "--warmup", "1")
     e, _ = bit_errors(1001)
     assert d["frames"] == 2 * 1001 and d["scaling"] == "strong" and d["bit_errors"] == 2 * e
+
+
+@pytest.fixture(scope="module")
+def wire_stream(tmp_path_factory):
+    """bench.py's config-4 stream (2048 D-config frames, gaps, CFO, 20 dB) as
+    the SDR's complex<int16> wire samples in a file, and the oracle's
+    sequential rx.cpp walk over it (its SDR ring, the library default)."""
+    import ofdm_synth as Y
+    p = dict(O.DEFAULT)
+    m = M.Modem(p, 0)
+    lay = Y.StreamLayout(p, 2048)
+    x16 = Y.stream_slice(m, lay, 0, lay.n, torch.device("cuda", 0), i16=True).cpu().numpy()
+    m.close()
+    path = tmp_path_factory.mktemp("stream") / "stream_i16.bin"
+    x16.tofile(path)
+    w = x16.astype(np.float64)
+    want = O.stream_walk_ring(p, w[0::2] + 1j * w[1::2])[0]
+    return str(path), lay.n, np.asarray(want, dtype=np.int64)
+
+
+@pytest.mark.skipif(not os.path.exists(APP), reason="ofdm_multigpu not built")
+@pytest.mark.parametrize("shards", [1, 2, 3, 8])
+def test_multigpu_app_sharded_stream_owns_the_sequential_walks_frames(wire_stream, shards, tmp_path):
+    # the C++ host's sharded stream receive (ofdm_stream_report_pack /
+    # ofdm_stream_stitch_plan, rows all-gathered through host memory: the
+    # ranks share the one GPU here; one rank per GPU uses ncclAllGather):
+    # the union of the owned frames, in stream order, is the oracle's walk
+    path, n, want = wire_stream
+    out = tmp_path / "pbs.bin"
+    d = run_app("--stream", path, "--shards", str(shards), "--gpus", "1", "--pbs-out", str(out), "--reps", "2")
+    got = np.fromfile(out, dtype=np.int64)
+    assert d["ranks"] == shards and d["stream_samples"] == n and d["frames"] == len(got)
+    assert d["exchange"].startswith("host memory") or shards == 1
+    assert np.array_equal(got, want)
+    assert d["value"] > 0
+
+
+@pytest.mark.skipif(not os.path.exists(APP), reason="ofdm_multigpu not built")
+def test_multigpu_app_sharded_stream_rewalks_stay_exact(wire_stream, tmp_path):
+    # a report cap of 1 frame: the ranks' reports carry only their first and
+    # last located frames, so speculative walks are rarely accepted and the
+    # plan makes ranks re-walk from their predecessor's exit state: still the
+    # oracle's walk
+    path, n, want = wire_stream
+    out = tmp_path / "pbs.bin"
+    d = run_app("--stream", path, "--shards", "6", "--gpus", "1", "--report-cap", "1", "--pbs-out", str(out))
+    assert np.array_equal(np.fromfile(out, dtype=np.int64), want)
+    assert d["rewalks"] >= 1  # the re-walk path ran
