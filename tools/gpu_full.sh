@@ -13,8 +13,10 @@ import json;d=json.load(open('gpurun_out/${TAG}_bench.json'))
 print('value', d['value']/1e9, 'ms', d['ms_per_step'], 'rx frac', d['roofline']['frac'], 'rx ms', d['roofline']['avg_launch_ms'], 'tx ms', d['tx_avg_launch_ms'])
 for k in ('stream','stream_int16'):
     s=d[k]; print(k, s['value']/1e9, s['ms_per_call'], s['roofline']['frac'], s['frames_found'], s['frames_error_free'], s['rewalks_per_call'], (s['cpu_baseline'] or {}).get('value'))
-    pp=s.get('pipelined'); print('  pipelined', pp and pp['value']/1e9, pp and pp['outputs_match_serial'], 'compute frac', s['compute']['frac'])
+    print('  compute frac', s['compute']['frac'], s['compute']['kernels_us'])
 b=d.get('stream_B')
 if b: print('stream_B', b['value']/1e9, b['ms_per_call'], b['frames_found'], b['frames_error_free'], 'staged', b['staged']['value']/1e9, b['staged']['ms_per_call'], 'speedup', b['staged']['fused_speedup_per_sample'])
+g=d.get('stream_ingest')
+if g: print('stream_ingest', g.get('value', 0)/1e9, g.get('ms_per_stream'), 'pcie', g.get('pcie_h2d'), 'frac', g.get('frac_of_pcie_ceiling'), 'equal', g.get('outputs_equal_device_resident_call'))
 c=d['config3']; print('config3', c['value']/1e9, c['roofline']['frac'])
 "
