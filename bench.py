@@ -595,7 +595,9 @@ def main():
                     help="contexts for the stream record's two-context figure (1: off, the default: one context "
                          "per GPU is the supported mode, INTEGRATION.md; one GPU only)")
     ap.add_argument("--no-ingest", action="store_true", help="skip the host-ingest stream sub-record")
-    ap.add_argument("--ingest-chunk", type=int, default=1 << 22, help="stream samples per ingest call")
+    ap.add_argument("--ingest-chunk", type=int, default=1 << 24,
+                    help="stream samples per ingest call (16 M: a call's walk latency, ~0.3 ms, hides behind the "
+                         "next chunk's ~1.2 ms PCIe copy; profiles/r06/ingest_chunk_sweep.jsonl)")
     ap.add_argument("--ingest-reps", type=int, default=3)
     ap.add_argument("--no-config3", action="store_true", help="skip the config-3 (config C) sub-record")
     ap.add_argument("--config3-frames", type=int, default=4096, help="config C frames per GPU (weak)")

@@ -2503,12 +2503,6 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
                         mbits |= ((k >= a.a1 && k <= a.b1) + (k >= a.a2 && k <= a.b2)) << (2 * i);
                     }
                 }
-                // int16 wire samples: the next step's 16 words (16 VGPRs) are
-                // requested before this step's transform, so their HBM round
-                // trip hides behind it (one dependent load per step less);
-                // discarded when the step hits or the scan stops
-                int nw[16];
-                bool pre = false;  // nw holds this step's words
                 for (long base = pos;; base += 2L * G * N) {
                     if (const int ss = scan_stop(base)) {
                         stop = ss == 1;
@@ -2533,38 +2527,6 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
                             for (int i = 0; i < 8; ++i) {
                                 va[i] = liveA ? make_float2((float)da[i].x, (float)da[i].y) : make_float2(0.f, 0.f);
                                 vb[i] = liveB ? make_float2((float)db[i].x, (float)db[i].y) : make_float2(0.f, 0.f);
-                            }
-                            pre = false;
-                        } else if constexpr (F == FMT_I16) {
-                            const int* p = reinterpret_cast<const int*>(a.iq16) + tt;
-                            int w[16];
-                            if (pre) {
-#pragma unroll
-                                for (int i = 0; i < 16; ++i) w[i] = nw[i];
-                            } else {
-                                const long oA = liveA ? bA : 0, oB = liveB ? bB : 0;
-#pragma unroll
-                                for (int i = 0; i < 8; ++i) {
-                                    w[i] = p[oA + T * i];
-                                    w[8 + i] = p[oB + T * i];
-                                }
-                            }
-                            // the next step's blocks, where they lie wholly in the
-                            // stream (else the next step reloads them itself)
-                            const long nA = bA + 2L * G * N, nB = bB + 2L * G * N;
-                            const long qA = nA >= 0 && nA + N <= a.n ? nA : 0, qB = nB >= 0 && nB + N <= a.n ? nB : 0;
-#pragma unroll
-                            for (int i = 0; i < 8; ++i) {
-                                nw[i] = p[qA + T * i];
-                                nw[8 + i] = p[qB + T * i];
-                            }
-                            pre = true;
-#pragma unroll
-                            for (int i = 0; i < 8; ++i) {
-                                va[i] = liveA ? make_float2((float)(short)(w[i] & 0xffff), (float)(w[i] >> 16))
-                                              : make_float2(0.f, 0.f);
-                                vb[i] = liveB ? make_float2((float)(short)(w[8 + i] & 0xffff), (float)(w[8 + i] >> 16))
-                                              : make_float2(0.f, 0.f);
                             }
                         } else {
                             load8_block32<T, F>(a, bA + tt, liveA, va);

@@ -24,9 +24,10 @@
  *     entry points (find_t2sin, find_preamble) and the stream receiver keep
  *     one scratch per ctx: a ctx has at most one of those calls in flight at
  *     a time (consecutive calls on one stream are always fine); overlapping
- *     them on two streams takes two contexts, as INTEGRATION.md's
- *     double-buffered receiver does. A stream call waits (on the device) for
- *     the previous stream call's decode when it is issued on another stream.
+ *     them on two streams takes two contexts (measured slower than one
+ *     context's back-to-back calls: INTEGRATION.md). A stream call waits (on
+ *     the device) for the previous stream call's decode when it is issued on
+ *     another stream.
  */
 #ifndef OFDM_MI355X_H
 #define OFDM_MI355X_H
