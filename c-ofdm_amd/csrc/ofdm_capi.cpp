@@ -140,6 +140,7 @@ struct ofdm_ctx {
     double2* d_preamble = nullptr; // ofdm_preamble (preamble_len)
     double2* d_templ = nullptr;    // pr_sin_len
     double2* d_tspec = nullptr;    // WALK_FFT_M template spectrum (stream walker FFT search)
+    float2* d_tspec32 = nullptr;   // the same rounded to FP32 (the search's FP32 tier)
     double2* d_twm = nullptr;      // WALK_FFT_M twiddles
     double tspec_max = 0.0;
     double2* d_modpre = nullptr;   // D*npr
@@ -344,7 +345,7 @@ int ofdm_destroy(ofdm_ctx* c)
     (void)hipSetDevice(c->device);
     void* ptrs[] = {c->d_tw, c->d_data_bin, c->d_data_slot, c->d_pilot_bin, c->d_bin_map, c->d_rx_pack,
                     c->d_pilot_swz, c->d_tx_code, c->d_const,
-                    c->d_const_bpsk, c->d_header, c->d_preamble, c->d_templ, c->d_tspec, c->d_twm, c->d_modpre,
+                    c->d_const_bpsk, c->d_header, c->d_preamble, c->d_templ, c->d_tspec, c->d_tspec32, c->d_twm, c->d_modpre,
                     c->d_t2mask,
                     c->d_t2tw, c->d_first, c->d_scratch, c->d_cfo_scratch, c->d_pre_hv, c->d_pre_done};
     for (void* q : ptrs)
@@ -598,7 +599,10 @@ int ofdm_create(const ofdm_params* params, int device, ofdm_ctx** out)
             twm = twiddles(M);
         }
         for (size_t i = 0; i < mp.size(); ++i) mp[i] = make_double2(c->mod_preamble[i].real(), c->mod_preamble[i].imag());
-        if ((!tsp.empty() && ((rc = upload(&c->d_tspec, tsp)) || (rc = upload(&c->d_twm, twm)))) ||
+        std::vector<float2> tsp32(tsp.size());
+        for (size_t k = 0; k < tsp.size(); ++k) tsp32[k] = make_float2((float)tsp[k].x, (float)tsp[k].y);
+        if ((!tsp.empty() && ((rc = upload(&c->d_tspec, tsp)) || (rc = upload(&c->d_tspec32, tsp32)) ||
+                              (rc = upload(&c->d_twm, twm)))) ||
             (rc = upload(&c->d_header, hdr)) || (rc = upload(&c->d_preamble, pre)) || (rc = upload(&c->d_templ, tpl)) ||
             (rc = upload(&c->d_modpre, mp)) || (rc = upload(&c->d_t2mask, c->t2_mask))) {
             ofdm_destroy(c);
@@ -1479,6 +1483,7 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
     w.tw_m = c->d_twm;
     w.tspec = c->d_tspec;  // nullptr: direct certified search
     w.tspec_max = c->tspec_max;
+    w.tspec32 = tu.pre_f32 ? c->d_tspec32 : nullptr;  // FP32 tier of the FFT search
     w.iq = reinterpret_cast<const double2*>(iq);
     w.iq16 = reinterpret_cast<const short2*>(iq16);
     w.n = nn;
@@ -2049,6 +2054,7 @@ int ofdm_walk_tuning_default(ofdm_walk_tuning* o)
     o->t2_f32 = 1;
     o->t2_margin = 4e-5;
     o->lookback = 1;
+    o->pre_f32 = 1;
     return OFDM_OK;
 }
 
@@ -2064,6 +2070,7 @@ int ofdm_set_walk_tuning(ofdm_ctx* c, const ofdm_walk_tuning* t)
     if (!c || !t) return fail(OFDM_ERR_INVALID, "null argument");
     if (t->staged_decode != 0 && t->staged_decode != 1) return fail(OFDM_ERR_INVALID, "staged_decode must be 0 or 1");
     if (t->lookback != 0 && t->lookback != 1) return fail(OFDM_ERR_INVALID, "lookback must be 0 or 1");
+    if (t->pre_f32 != 0 && t->pre_f32 != 1) return fail(OFDM_ERR_INVALID, "pre_f32 must be 0 or 1");
     if (t->chunks_per_slot < 1 || t->halo_milli < -1 || t->ext_milli < 0 || !(t->t2_margin >= 0.0) ||
         t->max_rec_cap < 0)
         return fail(OFDM_ERR_INVALID, "walk tuning out of range");

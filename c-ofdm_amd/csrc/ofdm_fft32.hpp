@@ -310,3 +310,154 @@ __device__ __forceinline__ void fft_regs_wave32p(PCx (&v)[8], int t, const doubl
 }
 
 }  // namespace ofdm
+
+namespace ofdm {
+
+// ---------------------------------------------------------------- one transform, packed
+// One FP32 transform with a point packed as {re, im} in a pf2: a complex add
+// is one v_pk_add_f32, a product by a twiddle two packed instructions (the
+// real part times {w.re, w.re}, then the swapped point times {-w.im, w.im}
+// added by v_pk_fma_f32 with swapped operand halves). Used by the stream
+// walker's FP32 tier of the FFT preamble search (ofdm_sync.hip
+// walk_preamble_fft): the correlation of a 512-sample window by two such
+// transforms, certified against its error bound like the FP64 form. The LDS
+// image keeps ofdm_fft.hpp's 16-B slots and swizzle (the point in the low 8
+// bytes): the walker is VALU-bound, not LDS-bound, and the swizzle stays
+// conflict-free.
+// Packed FP32 arithmetic with operand-half selection spelled out (VOP3P
+// op_sel / op_sel_hi / neg modifiers): the compiler does not fold the swaps
+// of shufflevector into the instruction and emitted a v_mov per swapped half
+// and a v_xor per negation (~125 extra VALU per 512-point transform pair).
+// On a 64-bit pair {lo, hi} of FP32, op_sel picks the source half of the lo
+// result, op_sel_hi that of the hi result.
+__device__ __forceinline__ pf2 c_mulw(pf2 a, pf2 w)  // a * w (complex)
+{
+    pf2 t, r;
+    // t = {a.re w.re, a.im w.re}
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(t) : "v"(a), "v"(w));
+    // r = {-a.im w.im + t.lo, a.re w.im + t.hi}
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[0,1,0]"
+        : "=v"(r) : "v"(a), "v"(w), "v"(t));
+    return r;
+}
+// x + SIGN i y
+template <int SIGN>
+__device__ __forceinline__ pf2 c_add_j(pf2 x, pf2 y)
+{
+    pf2 r;
+    if constexpr (SIGN > 0)  // {x.re - y.im, x.im + y.re}
+        asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(x), "v"(y));
+    else  // {x.re + y.im, x.im - y.re}
+        asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(x), "v"(y));
+    return r;
+}
+// x - SIGN i y
+template <int SIGN>
+__device__ __forceinline__ pf2 c_sub_j(pf2 x, pf2 y)
+{
+    return c_add_j<-SIGN>(x, y);
+}
+
+template <int SIGN>
+__device__ __forceinline__ void cdft4(pf2& a0, pf2& a1, pf2& a2, pf2& a3)
+{
+    const pf2 t0 = a0 + a2, t1 = a0 - a2;
+    const pf2 t2 = a1 + a3, d = a1 - a3;  // t3 = SIGN i d
+    a0 = t0 + t2;
+    a1 = c_add_j<SIGN>(t1, d);
+    a2 = t0 - t2;
+    a3 = c_sub_j<SIGN>(t1, d);
+}
+
+template <int SIGN>
+__device__ __forceinline__ void cdft8(pf2& x0, pf2& x1, pf2& x2, pf2& x3, pf2& x4, pf2& x5, pf2& x6, pf2& x7)
+{
+    constexpr float C = 0.70710678118654752440f;
+    const pf2 c2 = {C, C};
+    cdft4<SIGN>(x0, x2, x4, x6);
+    cdft4<SIGN>(x1, x3, x5, x7);
+    // O1 *= W8 = C (1 + SIGN i), O2 *= SIGN i, O3 *= W8^3 = C (-1 + SIGN i)
+    const pf2 o1 = c_add_j<SIGN>(x3, x3) * c2;
+    const pf2 o3 = c_sub_j<SIGN>(x7, x7) * (-c2);
+    const pf2 e0 = x0, e1 = x2, e2 = x4, e3 = x6, o0 = x1, y5 = x5;
+    x0 = e0 + o0;
+    x4 = e0 - o0;
+    x1 = e1 + o1;
+    x5 = e1 - o1;
+    x2 = c_add_j<SIGN>(e2, y5);  // e2 + o2, o2 = SIGN i x5
+    x6 = c_sub_j<SIGN>(e2, y5);
+    x3 = e3 + o3;
+    x7 = e3 - o3;
+}
+
+template <int LOGN, int R, int NS, int SIGN>
+__device__ __forceinline__ void stockham_pass32c(pf2 (&v)[8], int t, const double2* __restrict__ lds_tw,
+                                                 double2* __restrict__ lds, bool write)
+{
+    constexpr int N = 1 << LOGN, T = N / 8, B = 8 / R;
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+        const int b = t + T * u;
+        const int k = b & (NS - 1);
+        if constexpr (NS > 1) {
+            const double2 w64 = tw_get<LOGN, N / R>(lds_tw, k * (N / (NS * R)));
+            const pf2 w1 = {(float)w64.x, SIGN > 0 ? -(float)w64.y : (float)w64.y};
+            pf2 w = w1;
+            v[u + B] = c_mulw(v[u + B], w1);
+#pragma unroll
+            for (int r = 2; r < R; ++r) {
+                w = c_mulw(w, w1);
+                v[u + r * B] = c_mulw(v[u + r * B], w);
+            }
+        }
+        if constexpr (R == 8)
+            cdft8<SIGN>(v[u], v[u + B], v[u + 2 * B], v[u + 3 * B], v[u + 4 * B], v[u + 5 * B], v[u + 6 * B],
+                        v[u + 7 * B]);
+        else if constexpr (R == 4)
+            cdft4<SIGN>(v[u], v[u + B], v[u + 2 * B], v[u + 3 * B]);
+        if (!write) continue;
+        const int idxD = (b - k) * R + k;
+        float* img = reinterpret_cast<float*>(lds);
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            *reinterpret_cast<pf2*>(img + 4 * lds_swz(idxD + r * NS)) = v[u + r * B];
+    }
+}
+
+template <int LOGN, int PASS, int SIGN>
+__device__ __forceinline__ void fft_regs_tail_wave32c(pf2 (&v)[8], int t, const double2* __restrict__ lds_tw,
+                                                      double2* __restrict__ lds)
+{
+    using S = FftShape<LOGN>;
+    constexpr int T = S::T;
+    constexpr int NPASS = S::NPASS8 + (S::REM ? 1 : 0);
+    constexpr bool is8 = PASS < S::NPASS8;
+    constexpr int R = is8 ? 8 : (1 << S::REM);
+    constexpr int NS = 1 << (3 * PASS);
+    constexpr bool LAST = PASS == NPASS - 1;
+    static_assert(R == 8 || R == 4, "radix-8 / radix-4 passes");
+    wave_lds_sync();  // previous pass fully written
+    const float* img = reinterpret_cast<const float*>(lds);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = *reinterpret_cast<const pf2*>(img + 4 * lds_swz(t + T * i));
+    if constexpr (LAST) {
+        stockham_pass32c<LOGN, R, NS, SIGN>(v, t, lds_tw, lds, false);
+    } else {
+        wave_lds_sync();  // every lane has read before the image is overwritten
+        stockham_pass32c<LOGN, R, NS, SIGN>(v, t, lds_tw, lds, true);
+        fft_regs_tail_wave32c<LOGN, PASS + 1, SIGN>(v, t, lds_tw, lds);
+    }
+}
+
+// One N-point FP32 transform (v[i] = x[t + T*i] as {re, im}) by the T = N/8
+// <= 64 lanes of one wave, image lds (N 16-B slots); on exit v[i] = X[t + T*i].
+template <int LOGN, int SIGN>
+__device__ __forceinline__ void fft_regs_wave32c(pf2 (&v)[8], int t, const double2* __restrict__ lds_tw,
+                                                 double2* __restrict__ lds)
+{
+    static_assert(LOGN >= 6 && LOGN <= 9, "N/8 <= one wave");
+    stockham_pass32c<LOGN, 8, 1, SIGN>(v, t, lds_tw, lds, true);
+    fft_regs_tail_wave32c<LOGN, 1, SIGN>(v, t, lds_tw, lds);
+}
+
+}  // namespace ofdm

@@ -2065,7 +2065,17 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
         int out = INT_MAX;              // first certain PASS; -2 - lag: the first undecided lag
         constexpr double inv_m = 1.0 / M;
         const double lev2 = a.pr_level * a.pr_level;
-        for (int i0 = 0; i0 < C && out == INT_MAX; i0 += Q) {  // uniform
+        // One window's pass: the correlations of lags i0 .. i0 + nl - 1 by
+        // the FFT in FP64 or (F32) in packed FP32, their energies from the
+        // FP64 prefix sums; returns 0 when every lag is a certain FAIL, else
+        // the first lag that is not, as lag + 1 (a certain PASS) or -1 - lag
+        // (uncertain). The FP32 pass's transform error bound is the FP64
+        // pass's with u = 2^-24 (the inputs and tspec rounded to FP32 are
+        // inside its 1024 u ||x|| max|tspec| as well); its decisions are made
+        // in FP64, so an uncertain lag is re-decided by the FP64 pass of the
+        // same window, and only an FP64-uncertain lag goes to the exact search.
+        auto pass = [&](int i0, auto f32tag) -> int {
+            constexpr bool F32 = decltype(f32tag)::value;
             // opaque per-window copy of the lane: the addresses derived from
             // it are recomputed here, not hoisted out of the walk and held
             // live (spilled) across it
@@ -2111,33 +2121,51 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
             }
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) emax = fmax(emax, __shfl_xor(emax, o));
-            fft_regs_wave<LM, -1>(v, lane, tw_m, buf);  // X[lane + 64 i] (its LDS syncs publish P too)
             // Y = X . tspec (L2-resident table). The table address comes from
             // an opaque copy of the lane here: hoisted out of the walk loop,
             // the eight 64-bit addresses stayed live (and spilled) across it
-            {
-                int ln;
-                asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+            int ln;
+            asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+            if constexpr (F32) {
+                // the FP32 table (16 VGPRs) is requested before the forward
+                // transform, so its L2 round trip hides behind it
+                const float2* tp = a.tspec32 + ln;
+                float2 ts[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) ts[i] = tp[64 * i];
+                pf2 c[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) c[i] = pf2{(float)v[i].x, (float)v[i].y};
+                fft_regs_wave32c<LM, -1>(c, lane, tw_m, buf);  // X[lane + 64 i] (its LDS syncs publish P too)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) c[i] = c_mulw(c[i], pf2{ts[i].x, ts[i].y});
+                fft_regs_wave32c<LM, +1>(c, lane, tw_m, buf);  // c[j] = M e_{i0 + lane + 64 j} (P final: synced inside)
+                // parked in LDS (each lane its own entries, after its last read of the image)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) buf[lane + 64 * j] = make_double2((double)c[j].x, (double)c[j].y);
+            } else {
+                fft_regs_wave<LM, -1>(v, lane, tw_m, buf);  // X[lane + 64 i] (its LDS syncs publish P too)
                 const double2* tp = a.tspec + ln;
                 double2 ts[8];
 #pragma unroll
                 for (int i = 0; i < 8; ++i) ts[i] = tp[64 * i];
 #pragma unroll
                 for (int i = 0; i < 8; ++i) v[i] = cmul(v[i], ts[i]);
-            }
-            fft_regs_wave<LM, +1>(v, lane, tw_m, buf);  // v[j] = M e_{i0 + lane + 64 j} (P final: synced inside)
-            // parked in LDS (each lane its own entries, after its last read of
-            // the image), so the decisions below run as a rolled loop
+                fft_regs_wave<LM, +1>(v, lane, tw_m, buf);  // v[j] = M e_{i0 + lane + 64 j} (P final: synced inside)
+                // parked in LDS (each lane its own entries, after its last read of
+                // the image), so the decisions below run as a rolled loop
 #pragma unroll
-            for (int j = 0; j < 8; ++j) buf[lane + 64 * j] = v[j];
+                for (int j = 0; j < 8; ++j) buf[lane + 64 * j] = v[j];
+            }
             // every window sum of this window's lags is at most its total
             // energy (its samples lie inside the window): a bound on the
             // largest window sum without a pass over the lags
-            mrun = fmax(mrun, ptot);
-            erun = fmax(erun, emax);
-            const double Mall = (mrun + erun) * 1.0625;
+            const double mr = fmax(mrun, ptot), er = fmax(erun, emax);
+            const double Mall = (mr + er) * 1.0625;
             const double scan_err = (4.0 * R + 64.0) * U * ptot;
-            const double ef = 1024.0 * U * sqrt(ptot * 1.0625) * a.tspec_max;
+            const double uf = F32 ? 0x1.0p-24 : U;  // the transform's unit roundoff
+            const double ef = 1024.0 * uf * sqrt(ptot * 1.0625) * a.tspec_max;
+            int ret = 0;
 #pragma unroll 1  // rolled: it exits at the first decided lag
             for (int j = 0; j < 8; ++j) {
                 const int r = lane + 64 * j, i = i0 + r;
@@ -2162,11 +2190,22 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
                     const int l0 = __ffsll((long long)hitm) - 1;
                     const int d0 = __shfl(d, l0);
                     const int lag = i0 + 64 * j + l0;
-                    out = d0 == 1 ? lag : -2 - lag;
+                    ret = d0 == 1 ? lag + 1 : -1 - lag;
                     break;
                 }
             }
-            wave_lds_sync();  // every lane is done with buf / P before the next window overwrites them
+            wave_lds_sync();  // every lane is done with buf / P before the next pass overwrites them
+            if (ret >= 0) {   // decided (PASS) or all FAIL: the window counts toward the bounds
+                mrun = mr;
+                erun = er;
+            }
+            return ret;
+        };
+        for (int i0 = 0; i0 < C && out == INT_MAX; i0 += Q) {  // uniform
+            int r = a.tspec32 ? pass(i0, std::true_type{}) : -1;
+            if (r < 0) r = pass(i0, std::false_type{});  // no FP32 tier, or an FP32-uncertain lag
+            if (r > 0) out = r - 1;
+            else if (r < 0) out = -2 - (-1 - r);
         }
         if (t == 0) *res = out;
     }

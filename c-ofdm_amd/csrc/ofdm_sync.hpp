@@ -137,6 +137,7 @@ struct WalkArgs {
     const double2* tw_m;        // WALK_FFT_M forward twiddles
     const double2* tspec;       // sum_j c_j e^{+2 pi i k j / M}, k < M
     double tspec_max;           // max_k |tspec_k| (error bound)
+    const float2* tspec32;      // tspec rounded to FP32 (the FP32 tier of the FFT search), or nullptr
     // Look-back stitching on the device (lookback = 1; needs `queue`): chunk
     // c > 0 walks from its core start (minus halo) with no walk-in; past its
     // core end it checks each frame it locates against the records the

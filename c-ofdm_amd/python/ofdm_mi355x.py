@@ -59,7 +59,7 @@ class WalkTuning(C.Structure):
     _fields_ = [("chunks_per_slot", C.c_long), ("halo_milli", C.c_long), ("ext_milli", C.c_long),
                 ("exact_search", C.c_int), ("t2_f32", C.c_int), ("t2_margin", C.c_double),
                 ("allow_uncertified", C.c_int), ("staged_decode", C.c_int), ("lookback", C.c_int),
-                ("max_rec_cap", C.c_int)]
+                ("max_rec_cap", C.c_int), ("pre_f32", C.c_int)]
 
 
 class WalkState(C.Structure):

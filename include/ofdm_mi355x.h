@@ -543,6 +543,8 @@ typedef struct ofdm_walk_tuning {
     int max_rec_cap;      /* test only: > 0 caps the records per walker (forces
                              the look-back overflow and its halo-walk fallback;
                              default 0 = the computed bound)                    */
+    int pre_f32;          /* 1: certified FP32 tier of the FFT preamble search
+                             (an uncertain lag is re-decided in FP64; default 1) */
 } ofdm_walk_tuning;
 int ofdm_walk_tuning_default(ofdm_walk_tuning* out);
 int ofdm_get_walk_tuning(const ofdm_ctx* ctx, ofdm_walk_tuning* out);

@@ -265,6 +265,22 @@ def test_stream_walk_fp32_t2_screen_equals_fp64(tuning):
         check_against_oracle(cfg, x, screened)
 
 
+@pytest.mark.parametrize("ring", [None, 0], ids=["ring", "continuous"])
+def test_stream_walk_fp32_preamble_tier_equals_fp64(ring):
+    # the FFT preamble search's certified FP32 tier (pre_f32, the default)
+    # against the FP64 search alone: the same walk and outputs, on impaired
+    # streams and on a tx.cpp-style capture with exact-zero silences (windows
+    # of tiny energy, where the FP32 bound leaves lags uncertain and the FP64
+    # pass decides them)
+    for cfg, x in ((D, impaired_stream(D, 40, seed=4)[0]), (D, capture_stream(D, 60, seed=5)[0])):
+        tiered = run_stream(cfg, x, chunk=9000, ring=ring)
+        fp64 = run_stream(cfg, x, chunk=9000, ring=ring, tuning=dict(pre_f32=0))
+        assert tiered[0] == fp64[0]
+        for a, b in zip(tiered[1:], fp64[1:]):
+            assert np.array_equal(a, b)
+        check_against_oracle(cfg, x, tiered, ring=ring)
+
+
 def test_stream_calls_on_alternating_streams_one_context():
     # one ctx, stream calls issued on two HIP streams in turn without host
     # syncs between them: each call waits (on the device) for the previous
@@ -561,9 +577,11 @@ def test_walk_tuning_defaults_and_validation():
     assert t.staged_decode == 0
     with pytest.raises(M.OfdmError):
         m.walk_tuning(staged_decode=2)
-    assert t.max_rec_cap == 0
+    assert t.max_rec_cap == 0 and t.pre_f32 == 1
     with pytest.raises(M.OfdmError):
         m.walk_tuning(max_rec_cap=-1)
+    with pytest.raises(M.OfdmError):
+        m.walk_tuning(pre_f32=2)
     m.walk_tuning()  # back to the defaults
 
 
