@@ -1,12 +1,22 @@
 #!/bin/bash
 # scratch slot for one-off GPU commands (overwritten per experiment)
-# current: walker FP32 tier of the FFT preamble search: stream parity, same-box
-# A/B against the previous build, walker phase clocks
+# current: the round-6 profiling pass (headline trace + PMC, stream kernel
+# means + PMC, SQ counters of the stream kernels, the two-context overlap trace)
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
-TAG=${1:-r06f}
-timeout -k 10 900 python -u -m pytest tests/test_gpu_stream.py tests/test_gpu_stream_full.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/${TAG}_tests.log 2>&1 || { tail -40 gpurun_out/${TAG}_tests.log; exit 1; }
-tail -1 gpurun_out/${TAG}_tests.log
-TAG=$TAG LIBS="product abtest/libofdm_head.so" bash tools/stream_ab.sh || exit 1
-TUNINGS=chunks_per_slot=1 bash tools/gpu_walk_prof.sh
+bash tools/gpu_profile_round.sh || { echo profile_round failed; exit 1; }
+python3 -c "
+import json
+print(json.dumps(json.load(open('gpurun_out/trace_timed.json'))))
+for f in ('gpurun_out/pmc_rx.json','gpurun_out/pmc_tx.json'):
+    d=json.load(open(f)); print(f, d['traffic_over_algorithmic'])
+d=json.load(open('gpurun_out/bench.json'))
+print('bench', d['value']/1e9, d['ms_per_step'], d['roofline']['frac'], d['roofline']['avg_launch_ms'], d['tx_avg_launch_ms'])
+"
+bash tools/gpu_stream_trace.sh > gpurun_out/r06_stream_trace.log 2>&1 || { tail gpurun_out/r06_stream_trace.log; exit 1; }
+tail -40 gpurun_out/r06_stream_trace.log
+TAG=r06 bash tools/gpu_profile_stream.sh || exit 1
+bash tools/sq_stream.sh --frames 16384 --i16 && cp gpurun_out/sq_stream.txt gpurun_out/r06_sq_stream_Di16.txt && \
+bash tools/sq_stream.sh --frames 16384 && cp gpurun_out/sq_stream.txt gpurun_out/r06_sq_stream_D.txt || exit 1
+bash tools/gpu_stream_overlap.sh
