@@ -1586,7 +1586,8 @@ static int rx_stream_impl(ofdm_ctx* c, const double* iq, const int16_t* iq16, si
         HIP_TRY(hipFree(d_prof));
         if (FILE* f = fopen(prof_path, "a")) {
             fprintf(f, "{\"nchunks\": %ld, \"chunk\": %ld, \"lookback\": %d, \"grid\": %ld, \"fields\": "
-                       "[\"t0\", \"t_core\", \"t_end\", \"ext_frames\", \"waits\", \"block\", \"xcc\", \"nrec\"], "
+                       "[\"t0\", \"t_core\", \"t_end\", \"ext_frames\", \"waits\", \"block\", \"xcc\", \"nrec\", "
+                       "\"t2_ticks\", \"pre_ticks\", \"scan_steps\", \"fp64_evals\", \"searches\", \"hw_id\"], "
                        "\"chunks\": [", nchunks, chunk, (int)lbk, std::min(nchunks, slots));
             for (long k = 0; k < nchunks; ++k) {
                 fprintf(f, "%s[", k ? "," : "");

@@ -2739,8 +2739,10 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
     }
     if (t0 == 0) {
         if (long* prof = WALK_PROF) {
-            unsigned xcc;
+            unsigned xcc, hwid;
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+            prof[13] = (long)hwid;  // wave, SIMD, CU, SH, SE of this walker's first wave
             prof[2] = (long)wall_clock64();
             prof[5] = blockIdx.x;
             prof[6] = xcc & 0xf;

@@ -158,7 +158,7 @@ struct WalkArgs {
     // preamble searches}
     long* prof;
 };
-constexpr int WALK_PROF_FIELDS = 13;
+constexpr int WALK_PROF_FIELDS = 14;
 constexpr int WALK_PUB_DONE = 1 << 30;
 // set by a chunk's walker when it starts (with the count, until DONE): a
 // walker looks back on (waits for) only a chunk whose walker is running

@@ -51,6 +51,34 @@ def summarise(d):
             "fp64_evals_per_search": round(float(f64.sum()) / nf, 3),
             "searches_per_walker": round(float(nsearch.mean()), 2),
         }
+    if a.shape[1] >= 14:  # HW_ID: the CU each walker ran on; per CU, its walkers' work against its finish
+        hw = a[:, 13]
+        cu = (xcc << 8) | (((hw >> 13) & 7) << 5) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 15)
+        keys, inv = np.unique(cu, return_inverse=True)
+        fin = np.zeros(len(keys))
+        busy = np.zeros(len(keys))
+        first = np.full(len(keys), 1e30)
+        cnt = np.zeros(len(keys), np.int64)
+        np.maximum.at(fin, inv, end)
+        np.minimum.at(first, inv, end)
+        np.add.at(busy, inv, dur)
+        np.add.at(cnt, inv, 1)
+        simd = (hw >> 4) & 3
+        out["cus"] = {
+            "count": int(len(keys)), "walkers_per_cu": {int(k): int(v) for k, v in zip(*np.unique(cnt, return_counts=True))},
+            "finish_us_pct": q(fin), "first_walker_end_us_pct": q(first),
+            "walker_us_sum_per_cu_pct": q(busy),
+            "walkers_per_simd": {int(k): int(v) for k, v in zip(*np.unique(simd, return_counts=True))},
+            # how much of the span the CU had all its walkers running: mean end / finish
+            "mean_end_over_finish": round(float(np.mean([end[inv == i].mean() / fin[i] for i in range(len(keys))])), 3),
+            "corr_finish_vs_frames": round(float(np.corrcoef(fin, np.bincount(inv, weights=nrec))[0, 1]), 3),
+        }
+        # walker duration by its dispatch rank on its CU (block order)
+        rank = np.zeros(len(a), np.int64)
+        for i in range(len(keys)):
+            m = np.nonzero(inv == i)[0]
+            rank[m[np.argsort(blk[m])]] = np.arange(len(m))
+        out["cus"]["walker_us_by_dispatch_rank"] = [round(float(dur[rank == r].mean()), 1) for r in range(int(rank.max()) + 1)]
     return out
 
 
