@@ -7,7 +7,7 @@ timeout -k 10 1200 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeou
 tail -1 gpurun_out/${TAG}_gpu_tests.log
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || { cat gpurun_out/${TAG}_smoke.log; exit 1; }
 grep smoke gpurun_out/${TAG}_smoke.log
-timeout -k 10 400 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { tail gpurun_out/${TAG}_bench.err; exit 1; }
+timeout -k 10 400 python bench.py ${BENCH_ARGS} > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { tail gpurun_out/${TAG}_bench.err; exit 1; }
 python3 -c "
 import json;d=json.load(open('gpurun_out/${TAG}_bench.json'))
 print('value', d['value']/1e9, 'ms', d['ms_per_step'], 'rx frac', d['roofline']['frac'], 'rx ms', d['roofline']['avg_launch_ms'], 'tx ms', d['tx_avg_launch_ms'])
