@@ -2676,7 +2676,10 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
         // ring mode: the state after the frame, (pb + msg, rend), is one of
         // two; the record says which (a frame before the stream's first
         // sample is kept as is: the host rejects it)
-        const long rv = (ring && pb >= 0 && rend != ring_after(pb + a.msg)) ? (pb | WALK_REC_LAG) : pb;
+        // (rend is a ring end, so rend == ring_after(q) exactly when q lies in
+        // [rend - ring, rend): no 64-bit division per frame)
+        const long qn = pb + a.msg;
+        const long rv = (ring && pb >= 0 && !(qn >= rend - a.ring && qn < rend)) ? (pb | WALK_REC_LAG) : pb;
         if (t == 0 && nrec < a.max_rec) {
             long* rp = a.rec + (long)c * a.max_rec + nrec;
             if (lb) {
