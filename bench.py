@@ -265,11 +265,14 @@ def stream_leg(args, dist, dev, world, rank, M, i16: bool, p=None, frames_per_gp
     phases = []
     modem.stream_timing(True)
     try:
+        # every rank makes all three calls (each holds the report
+        # all-gather): a call without timed phases is skipped, not the rest
         for _ in range(3):
             rx.run(walk, exchange)
-            phases.append(modem.last_stream_times())
-    except M.OfdmError:
-        phases = []  # no timed decode (e.g. a shard whose call took the halo walk)
+            try:
+                phases.append(modem.last_stream_times())
+            except M.OfdmError:
+                pass  # no timed decode (e.g. a shard whose call took the halo walk)
     finally:
         modem.stream_timing(False)
     torch.cuda.synchronize(dev)
