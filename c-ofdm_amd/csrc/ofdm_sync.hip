@@ -2084,6 +2084,7 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
             const int nl = min(Q, C - i0), W = nl + L - 1;
             const long s0 = s + i0;
             double2 v[8];
+            OFDM_PHASE(pre_window_load);
             load8_window<F>(a, s0, lane, W, v);
             double emax = 0.0;
 #pragma unroll
@@ -2121,6 +2122,7 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
             }
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) emax = fmax(emax, __shfl_xor(emax, o));
+            OFDM_PHASE(pre_transforms);
             // Y = X . tspec (L2-resident table). The table address comes from
             // an opaque copy of the lane here: hoisted out of the walk loop,
             // the eight 64-bit addresses stayed live (and spilled) across it
@@ -2157,6 +2159,7 @@ __device__ int walk_preamble_fft(const WalkArgs& a, long s, double2* buf, double
 #pragma unroll
                 for (int j = 0; j < 8; ++j) buf[lane + 64 * j] = v[j];
             }
+            OFDM_PHASE(pre_decisions);
             // every window sum of this window's lags is at most its total
             // energy (its samples lie inside the window): a bound on the
             // largest window sum without a pass over the lags
@@ -2408,6 +2411,7 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
             }
             if (past || pos >= end + a.ext) break;
         }
+        OFDM_PHASE(walk_frame_top);
         const long spos = pos, srend = rend;  // this step's start state
         {
             // issue priority by the work left: walkers further from their
@@ -2551,6 +2555,7 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
                     int tt;  // opaque per-step copy (see t2_eval64)
                     asm volatile("v_mov_b32 %0, %1" : "=v"(tt) : "v"(tt0));
                     if (long* prof = WALK_PROF; prof && t == 0) ++prof[10];
+                    OFDM_PHASE(t2_step32_load);
                     const long bA = base + (long)g * N, bB = bA + (long)G * N;
                     const bool liveA = ring ? (bA + N <= rend && bA < a.n) : bA + N <= a.n;
                     const bool liveB = ring ? (bB + N <= rend && bB < a.n) : bB + N <= a.n;
@@ -2574,7 +2579,9 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
 #pragma unroll
                         for (int i = 0; i < 8; ++i) v[i] = PCx{pf2{va[i].x, vb[i].x}, pf2{va[i].y, vb[i].y}};
                     }
+                    OFDM_PHASE(t2_step32_fft);
                     fft_regs_wave32p<LOGT, -1>(v, tt, lds_tw, fftb32 + g * N);
+                    OFDM_PHASE(t2_step32_sums);
                     // per block: total energy and detector-bin energy (packed A | B)
                     pf2 tot2 = {0.f, 0.f}, sin2 = {0.f, 0.f};
                     int mb;
@@ -2645,6 +2652,7 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
             }
         }
         if (long* prof = WALK_PROF; prof && t == 0) prof[8] += (long)wall_clock64() - prof_t2;
+        OFDM_PHASE(walk_after_scan);
         if (stop) break;
         if (miss) {  // rx.cpp:137-145: pos = output_size of the next buffer
             pos = rend;
@@ -2653,6 +2661,7 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
         }
         if (ring && hit >= rend - a.out_len) rend += a.ring;  // rx.cpp:147-156: carry, next buffer
         const long prof_pre = PROF ? (long)wall_clock64() : 0;
+        OFDM_PHASE(walk_preamble_call);
         const int lag = (a.tspec && !a.exact_only)
                             ? walk_preamble_fft<WT, F>(a, hit, big, P, tw_m, reinterpret_cast<int*>(scr + 2), xs, normv,
                                                     best, t)
@@ -2661,6 +2670,7 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
             prof[9] += (long)wall_clock64() - prof_pre;
             ++prof[12];
         }
+        OFDM_PHASE(walk_record);
         // rx.cpp:160-168: find_preamble's -10 (no lag passes) moves on by a
         // message. rx.cpp tests preamble_begin < -2 in buffer coordinates,
         // where a found preamble gives >= 1; in stream coordinates a found
