@@ -2572,6 +2572,12 @@ __global__ void __launch_bounds__(WalkShape<LOGT>::WT, 4) stream_walk_kernel(Wal
                                 va[i] = liveA ? make_float2((float)da[i].x, (float)da[i].y) : make_float2(0.f, 0.f);
                                 vb[i] = liveB ? make_float2((float)db[i].x, (float)db[i].y) : make_float2(0.f, 0.f);
                             }
+                        } else if (F == FMT_I16 && __all(liveA && liveB)) {
+                            // int16: every block of the step live (the rule), no selects
+                            // (int16 walker 231 -> 228 us same box, profiles/r06/ab_walker_int16_all_live_loads.txt;
+                            // the f64 instantiation spilled with it: 298 -> 303 us)
+                            load8_block32<T, F>(a, bA + tt, true, va);
+                            load8_block32<T, F>(a, bB + tt, true, vb);
                         } else {
                             load8_block32<T, F>(a, bA + tt, liveA, va);
                             load8_block32<T, F>(a, bB + tt, liveB, vb);
